@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Regenerate the golden vectors under tests/golden/ from the *reference itself*.
+
+Runs oracle/_ref/ref_harness (the reference's header-only WharfMH compiled by
+``make -C oracle ref`` from /root/reference, unmodified) and packages its dumps
+as small fixtures.  Only runs in the build container (the reference is not on
+the GPU box); the committed outputs are data: inputs and the reference's
+outputs for them.
+
+    python tests/golden/make_golden.py            # writes tests/golden/*
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+WIKI = "/root/reference/experiments/data/wiki-graph"   # SNAP edge list shipped with the reference
+SENT = 0xFFFFFFFE
+
+
+def run(args, env_threads=1):
+    env = dict(os.environ, NUM_THREADS=str(env_threads))
+    r = subprocess.run([HARNESS] + [str(a) for a in args], env=env, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"harness failed ({r.returncode}): {r.stderr[-2000:]}")
+    return r.stdout
+
+
+def snap_to_csr(path):
+    """SNAPtoAdj -s equivalent: symmetrise, sort, drop duplicates and self loops
+    (reproduces the 2405 V / 23192 E the survey measured for wiki-graph)."""
+    e = np.loadtxt(path, dtype=np.int64).reshape(-1, 2)
+    s = np.concatenate([e, e[:, ::-1]])
+    s = s[s[:, 0] != s[:, 1]]
+    u = np.unique(s, axis=0)
+    n = int(u.max()) + 1
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(np.bincount(u[:, 0], minlength=n), out=off[1:])
+    return off, u[:, 1].astype(np.uint32)
+
+
+def write_csr(path, off, adj):
+    with open(path, "wb") as f:
+        np.array([len(off) - 1, len(adj)], dtype=np.uint64).tofile(f)
+        off[:-1].astype(np.uint64).tofile(f)
+        adj.astype(np.uint32).tofile(f)
+
+
+def read_walks(d, tag, L):
+    return np.fromfile(os.path.join(d, f"walks_{tag}.bin"), dtype=np.uint32).reshape(-1, L)
+
+
+def read_index(d, tag):
+    raw = open(os.path.join(d, f"index_{tag}.bin"), "rb").read()
+    n = int(np.frombuffer(raw[:8], dtype=np.uint64)[0])
+    cnt = np.frombuffer(raw[8:8 + 8 * n], dtype=np.uint64).copy()
+    body = np.frombuffer(raw[8 + 8 * n:], dtype=np.uint32).reshape(-1, 2)
+    return cnt, body[:, 0].copy(), body[:, 1].copy()
+
+
+def read_graph(d, tag):
+    raw = open(os.path.join(d, f"graph_{tag}.bin"), "rb").read()
+    n = int(np.frombuffer(raw[:8], dtype=np.uint64)[0])
+    off = np.frombuffer(raw[8:8 + 8 * (n + 1)], dtype=np.uint64).copy()
+    adj = np.frombuffer(raw[8 + 8 * (n + 1):], dtype=np.uint32).copy()
+    return off, adj
+
+
+def rd(d, name, dt=np.uint32):
+    return np.fromfile(os.path.join(d, name), dtype=dt)
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def mh_class_fractions(walks, off, adj):
+    """Per-transition class of walk[pos+1] given (walk[pos-1], walk[pos]), pos >= 1:
+    return (== prev), triangle (edge prev-next), outward (otherwise)."""
+    ret = tri = out = 0
+    adjset = {}
+    for v in range(len(off) - 1):
+        adjset[v] = set(adj[off[v]:off[v + 1]].tolist())
+    for w in walks:
+        for pos in range(1, len(w) - 1):
+            a, b, c = int(w[pos - 1]), int(w[pos]), int(w[pos + 1])
+            if c == SENT:
+                break
+            if c == a:
+                ret += 1
+            elif c in adjset[a]:
+                tri += 1
+            else:
+                out += 1
+    t = ret + tri + out
+    return {"return": ret / t, "triangle": tri / t, "outward": out / t, "transitions": t}
+
+
+def main():
+    if not os.path.exists(HARNESS):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
+    tmp = tempfile.mkdtemp(prefix="golden_")
+    meta = {"generator": "tests/golden/make_golden.py via oracle/_ref/ref_harness (reference headers, unmodified)"}
+    try:
+        # ---- 1. known answers: RNG, hashes, Szudzik, RMAT batches ---------------
+        batches = [(8, 64, 0, 1), (100, 1024, 3, 1), (500, 2048, 5, 0), (5000, 2405, 0, 1), (2000, 4096, 11, 0)]
+        args = ["out", tmp, "kat"]
+        for b in batches:
+            args += ["batch"] + list(b)
+        run(args)
+        shutil.copy(os.path.join(tmp, "kat.txt"), os.path.join(HERE, "kat.txt"))
+        bz = {}
+        for (M, V, s, d) in batches:
+            bz[f"b_{M}_{V}_{s}_{d}"] = rd(tmp, f"batch_gen_{M}_{V}_{s}_{d}.bin").reshape(-1, 2)
+        np.savez_compressed(os.path.join(HERE, "rmat_batches.npz"), **bz)
+
+        # ---- 2. six-vertex graph (tests/sampler.cpp:24-35) -------------------------
+        six = {0: [1, 2], 1: [0, 2, 3], 2: [0, 1, 3, 4, 5], 3: [1, 2, 5], 4: [2, 5], 5: [2, 3, 4]}
+        off = np.zeros(7, dtype=np.uint64)
+        adj = []
+        for v in range(6):
+            adj += six[v]
+            off[v + 1] = len(adj)
+        adj = np.array(adj, dtype=np.uint32)
+        write_csr(os.path.join(tmp, "six.csr"), off, adj)
+        d6 = os.path.join(tmp, "six")
+        os.makedirs(d6)
+        run(["out", d6, "cfg", 2, 5, "deepwalk", 4, 1, "weight", 1, 7, "graph-csr", os.path.join(tmp, "six.csr"),
+             "gen", "dump-index", "walkstr", 0, "walkstr", 11])
+        d6n = os.path.join(tmp, "six_n2v")
+        os.makedirs(d6n)
+        run(["out", d6n, "cfg", 2, 5, "node2vec", 0.5, 2, "weight", 1, 7, "graph-csr", os.path.join(tmp, "six.csr"), "gen"])
+        cnt, keys, nexts = read_index(d6, "0")
+        np.savez_compressed(os.path.join(HERE, "six.npz"), off=off, adj=adj, walks=read_walks(d6, "0_gen", 5),
+                            walks_node2vec=read_walks(d6n, "0_gen", 5), index_counts=cnt, index_keys=keys,
+                            index_nexts=nexts)
+        meta["six_walkstr"] = {"0": open(os.path.join(d6, "walkstr_0.txt")).read(),
+                               "11": open(os.path.join(d6, "walkstr_11.txt")).read()}
+
+        # ---- 3. RMAT scale-10 streaming case (wpv=2, L=20) --------------------------
+        # base: generate_batch_of_edges(12800, 2048, seed 1, undirected) on n = 1024
+        for model in ("deepwalk", "node2vec"):
+            dr = os.path.join(tmp, f"rmat10_{model}")
+            os.makedirs(dr)
+            out = run(["out", dr, "cfg", 2, 20, model, 0.5, 2, "weight", 1, 7, "graph-rmat", 12800, 2048, 1, 1024,
+                       "gen", "dump-index", "dump-graph",
+                       "ins", 500, 5, 0, "dump-index", "dump-graph",
+                       "del", 500, 5, 0, "dump-index", "dump-graph",
+                       "ins", 300, 9, 0, "dump-graph",
+                       "del", 200, 2, 0, "dump-graph"])
+            meta[f"rmat10_{model}_log"] = out
+        dr = os.path.join(tmp, "rmat10_deepwalk")
+        z = {}
+        for tag in ("0", "1", "2", "3", "4"):
+            o, a = read_graph(dr, tag)
+            z[f"off_{tag}"], z[f"adj_{tag}"] = o, a
+        for tag, name in (("0_gen", "gen"), ("1_ins", "ins1"), ("2_del", "del2"), ("3_ins", "ins3"), ("4_del", "del4")):
+            z[f"walks_{name}"] = read_walks(dr, tag, 20)
+        for tag in ("1_ins", "2_del", "3_ins", "4_del"):
+            z[f"batch_{tag}"] = rd(dr, f"batch_{tag}_in.bin").reshape(-1, 2)
+            z[f"affected_{tag}"] = rd(dr, f"affected_{tag}.bin")
+        for tag in ("0", "1", "2"):
+            c, k, nx = read_index(dr, tag)
+            z[f"index_counts_{tag}"], z[f"index_keys_{tag}"], z[f"index_nexts_{tag}"] = c, k, nx
+        drn = os.path.join(tmp, "rmat10_node2vec")
+        for tag, name in (("0_gen", "gen"), ("1_ins", "ins1"), ("2_del", "del2")):
+            z[f"n2v_walks_{name}"] = read_walks(drn, tag, 20)
+        np.savez_compressed(os.path.join(HERE, "rmat10.npz"), **z)
+
+        # ---- 4. directed batches (throughput-latency.cpp:121 pattern) ----------------
+        dd = os.path.join(tmp, "rmat10_dir")
+        os.makedirs(dd)
+        try:
+            out = run(["out", dd, "cfg", 2, 20, "deepwalk", 4, 1, "weight", 1, 7, "graph-rmat", 12800, 2048, 1, 1024,
+                       "gen", "ins", 50, 0, 1, "del", 50, 0, 1])
+            zd = {"walks_gen": read_walks(dd, "0_gen", 20), "walks_ins": read_walks(dd, "1_ins", 20),
+                  "walks_del": read_walks(dd, "2_del", 20),
+                  "batch_ins": rd(dd, "batch_1_ins_in.bin").reshape(-1, 2),
+                  "affected_ins": rd(dd, "affected_1_ins.bin"), "affected_del": rd(dd, "affected_2_del.bin")}
+            np.savez_compressed(os.path.join(HERE, "rmat10_directed.npz"), **zd)
+            meta["rmat10_directed_log"] = out
+        except RuntimeError as ex:
+            meta["rmat10_directed_error"] = str(ex)
+
+        # ---- 5. wiki-graph (experiments/data/wiki-graph, SNAPtoAdj -s) ------------------
+        woff, wadj = snap_to_csr(WIKI)
+        np.savez_compressed(os.path.join(HERE, "wiki_csr.npz"), off=woff, adj=wadj)
+        write_csr(os.path.join(tmp, "wiki.csr"), woff, wadj)
+        dw = os.path.join(tmp, "wiki")
+        os.makedirs(dw)
+        out = run(["out", dw, "cfg", 10, 80, "deepwalk", 4, 1, "weight", 1, 7, "graph-csr", os.path.join(tmp, "wiki.csr"),
+                   "gen", "ins", 5000, 0, 0, "del", 5000, 0, 0, "walkstr", 12345])  # serial: the rewalk-point min-update races at >1 thread (wharfmh.h:524-536)
+        w, wz = {}, {}
+        for tag in ("0_gen", "1_ins", "2_del"):
+            wm = read_walks(dw, tag, 80)
+            w[tag] = {"sha256": sha(wm)}
+            wz[f"first64_{tag}"] = wm[:64]
+        for tag in ("1_ins", "2_del"):
+            a = rd(dw, f"affected_{tag}.bin")
+            w[f"affected_{tag}"] = {"count": int(len(a)), "sha256": sha(a)}
+            wz[f"batch_{tag}"] = rd(dw, f"batch_{tag}_in.bin").reshape(-1, 2)
+        np.savez_compressed(os.path.join(HERE, "wiki_golden.npz"), **wz)
+        w["walkstr_12345"] = open(os.path.join(dw, "walkstr_12345.txt")).read()
+        w["log"] = out
+        meta["wiki"] = w
+
+        # ---- 6. MH-mode statistics (reference, serial, config::random.reinit(42)) -------
+        mh = {}
+        for model, p, q in (("node2vec", 0.5, 2.0), ("deepwalk", 1.0, 1.0)):
+            dm = os.path.join(tmp, f"mh_{model}")
+            os.makedirs(dm)
+            run(["out", dm, "cfg", 10, 80, model, p, q, "weight", 0, 42, "graph-csr", os.path.join(tmp, "wiki.csr"), "gen"])
+            wm = read_walks(dm, "0_gen", 80)
+            st = mh_class_fractions(wm, woff, wadj)
+            # DeepWalk: uniform-neighbour check, per-(cur) next-vertex chi-square
+            if model == "deepwalk":
+                cnt = {}
+                for row in wm:
+                    for a, b in zip(row[:-1], row[1:]):
+                        if b == SENT:
+                            break
+                        cnt[(int(a), int(b))] = cnt.get((int(a), int(b)), 0) + 1
+                chi, dof = 0.0, 0
+                for v in range(len(woff) - 1):
+                    d = int(woff[v + 1] - woff[v])
+                    if d < 2:
+                        continue
+                    nb = wadj[woff[v]:woff[v + 1]]
+                    obs = np.array([cnt.get((v, int(x)), 0) for x in nb], dtype=np.float64)
+                    tot = obs.sum()
+                    if tot < 5 * d:
+                        continue
+                    exp = tot / d
+                    chi += float(((obs - exp) ** 2 / exp).sum())
+                    dof += d - 1
+                st["chi2"] = chi
+                st["dof"] = dof
+            mh[f"{model}_p{p}_q{q}"] = st
+        meta["mh_stats_reference"] = mh
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("golden vectors written to", HERE)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
