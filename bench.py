@@ -1,0 +1,252 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MH walk-steps/s for initial walk generation on the
+com-orkut-sized RMAT graph (BASELINE.json configs[1]: DeepWalk MH sampler,
+10 walks/vertex, length 80), plus the re-walk latency of 10k-edge batches.
+
+    python bench.py [--gpus N --steps K --warmup W]
+
+N > 1 is launched by torch.distributed.run, one rank per GPU: every rank holds
+the replicated CSR and owns a contiguous start-vertex range of the walks
+(balanced by non-isolated start vertices); the timed step has no collective.
+
+A "step" = one generate_initial_random_walks() over the whole graph (all
+ranks' shards).  value = transitions appended by all ranks per second.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+BYTES_PER_STEP_DEEPWALK = 24     # offsets/deg record 16 B + 1 target 4 B + 1 output 4 B
+ORKUT_EDGES = 117_185_083        # com-orkut undirected edge count (configs[1])
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--scale", type=int, default=22)
+    p.add_argument("--samples", type=int, default=ORKUT_EDGES)
+    p.add_argument("--seed", type=int, default=2)
+    p.add_argument("--wpv", type=int, default=10)
+    p.add_argument("--length", type=int, default=80)
+    p.add_argument("--model", choices=["deepwalk", "node2vec"], default="deepwalk")
+    p.add_argument("--paramP", type=float, default=0.5)
+    p.add_argument("--paramQ", type=float, default=2.0)
+    p.add_argument("--det", action="store_true", help="deterministic mode instead of MH")
+    p.add_argument("--rewalk-batches", type=int, default=3, help="10k-edge insert batches timed after the bench")
+    p.add_argument("--cpu-baseline", choices=["auto", "reference", "port", "off"], default="auto")
+    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--cpu-timeout", type=int, default=300)
+    return p.parse_args()
+
+
+def balanced_shards(deg: np.ndarray, parts: int):
+    """contiguous start-vertex ranges with equal numbers of non-isolated vertices"""
+    act = np.cumsum(deg > 0)
+    total = int(act[-1]) if len(act) else 0
+    bounds = [0]
+    for k in range(1, parts):
+        bounds.append(int(np.searchsorted(act, (total * k) // parts, side="right")))
+    bounds.append(len(deg))
+    return [(bounds[i], bounds[i + 1]) for i in range(parts)]
+
+
+def load_traffic(tag: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(REPO, "profiles", f"pmc_{tag}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_cores(requested: int) -> int:
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except Exception:
+        avail = os.cpu_count() or 1
+    return max(1, min(requested or 16, avail))
+
+
+def cpu_baseline(args, n, active_vertices, off, adj, kind):
+    """Reference CPU path (oracle/_ref/ref_harness, the reference's own headers)
+    on a bounded sample: the same RMAT graph, 1 walk per vertex (1/10 of the
+    workload's walks), same length and model, MH mode, timed generate only."""
+    cores = cpu_cores(args.cpu_threads)
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if kind in ("auto", "reference") and os.path.exists(harness):
+        cmd = [harness, "cfg", "1", str(args.length), args.model, str(args.paramP), str(args.paramQ), "weight",
+               "1" if args.det else "0", "42",
+               "graph-rmat", str(args.samples), str(2 * n), str(args.seed), str(n), "time-gen", "1"]
+        env = dict(os.environ, NUM_THREADS=str(cores))
+        log(f"cpu_baseline: reference harness, {cores} threads: {' '.join(cmd[1:])}")
+        try:
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.cpu_timeout)
+            m = re.search(r"time-gen seconds=([0-9.]+)", r.stdout)
+            if r.returncode == 0 and m:
+                secs = float(m.group(1))
+                steps = active_vertices * (args.length - 1)
+                return {"value": steps / secs, "unit": "walk-steps/s", "cores": cores, "kind": "reference",
+                        "sample": f"reference WharfMH::generate_initial_random_walks on the same RMAT graph "
+                                  f"(n={n}), walks_per_vertex=1 (1/{args.wpv} of the workload), L={args.length}, "
+                                  f"{'deterministic' if args.det else 'MH'} {args.model}; {steps} steps in {secs:.2f} s",
+                        "seconds": secs}
+            log("cpu_baseline: harness failed", r.returncode, r.stderr[-500:])
+        except subprocess.TimeoutExpired:
+            log("cpu_baseline: harness timed out")
+        if kind == "reference":
+            return None
+    # the C restatement (oracle/wharf_oracle.c), OpenMP over walks, same graph, bounded walk range
+    from oracle import oracle as O
+    eng = O.Engine(off, adj, wpv=args.wpv, L=args.length, model=O.NODE2VEC if args.model == "node2vec" else O.DEEPWALK,
+                   p=args.paramP, q=args.paramQ, deterministic=args.det, seed=0x5EED)
+    w1 = min(n * args.wpv, 2_000_000)
+    secs = eng.time_generate_range(0, w1, cores)
+    steps = eng.steps
+    return {"value": steps / secs, "unit": "walk-steps/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/wharf_oracle.c restatement, same graph, walks [0, {w1}), L={args.length}; "
+                      f"{steps} steps in {secs:.2f} s", "seconds": secs}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import dynamicgraphrepresentationlearning_amd as W
+
+    n = 1 << args.scale
+    cfg = W.WharfConfig(walks_per_vertex=args.wpv, walk_length=args.length,
+                        model=W.NODE2VEC if args.model == "node2vec" else W.DEEPWALK,
+                        paramP=args.paramP, paramQ=args.paramQ, deterministic=args.det, seed=0x5EED)
+    t0 = time.time()
+    g = W.WharfMH.from_rmat(n, args.samples, 2 * n, seed=args.seed, config=cfg, device=local)
+    off, adj = g.flatten_graph() if rank == 0 else (None, None)
+    off_np = off if off is not None else g.flatten_graph()[0]
+    deg = np.diff(off_np.astype(np.int64))
+    lo, hi = balanced_shards(deg, world)[rank]
+    g.set_shard(lo, hi)
+    m = g.number_of_edges()
+    log(f"[rank {rank}] graph n={n} m={m} built in {time.time() - t0:.1f}s; shard [{lo},{hi})")
+
+    def barrier():
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(local)
+
+    for i in range(args.warmup):
+        g.generate_initial_random_walks()
+        log(f"[rank {rank}] warmup {i}: {g.stats()['last_walk_kernel_ms']:.1f} ms")
+    barrier()
+    t_start = time.perf_counter()
+    kern_ms = []
+    for i in range(args.steps):
+        g.generate_initial_random_walks()
+        kern_ms.append(g.stats()["last_walk_kernel_ms"])
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    st = g.stats()
+    steps_local = st["steps"]
+    steps_total, t_max = steps_local, elapsed
+    if dist:
+        tt = torch.tensor([float(steps_local), elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        s = tt.clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        mx = tt.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        steps_total, t_max = int(s[0].item()), mx[1].item()
+    value = steps_total * args.steps / t_max
+    avg_kernel_ms = float(np.mean(kern_ms))
+    bytes_per_step = BYTES_PER_STEP_DEEPWALK if args.model == "deepwalk" else None
+    tag = f"gen_{args.model}_{'det' if args.det else 'mh'}_s{args.scale}"
+
+    # re-walk latency: 10k-edge batches (generate_batch_of_edges(5000, n, b, false, undirected))
+    rewalk = None
+    if args.rewalk_batches > 0:
+        lat, aff, gu, wu = [], [], [], []
+        for b in range(args.rewalk_batches):
+            batch = W.generate_batch_of_edges(5000, n, b, False, False, device=local)
+            barrier()
+            t1 = time.perf_counter()
+            a = g.insert_edges_batch(batch, remove_dups=True)
+            barrier()
+            lat.append((time.perf_counter() - t1) * 1e3)
+            s2 = g.stats()
+            aff.append(len(a))
+            gu.append(s2["last_graph_update_ms"])
+            wu.append(s2["last_walk_update_ms"])
+        rewalk = {"batches": args.rewalk_batches, "edges_per_batch": int(len(batch)),
+                  "latency_ms": [round(x, 3) for x in lat], "median_ms": round(float(np.median(lat)), 3),
+                  "affected_walks_rank": aff, "graph_update_ms": [round(x, 3) for x in gu],
+                  "walk_update_ms": [round(x, 3) for x in wu]}
+
+    if rank == 0:
+        achieved = (steps_local * bytes_per_step / (avg_kernel_ms * 1e-3) / 1e9) if bytes_per_step else None
+        traffic = load_traffic(tag)
+        line = {
+            "metric": "MH walk-steps/sec" if not args.det else "deterministic walk-steps/sec",
+            "value": round(value, 1),
+            "unit": "walk-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic RMAT (utility::generate_batch_of_edges semantics, a=.5 b=.2 c=.1), built on device",
+            "config": {"workload": f"configs[1] com-orkut-sized initial walk generation: RMAT scale {args.scale} "
+                                   f"(n={n}), {args.samples} undirected samples (seed {args.seed}) -> m={m} CSR "
+                                   f"entries; {args.model} {'deterministic' if args.det else 'MH'}, "
+                                   f"walks_per_vertex={args.wpv}, walk_length={args.length}",
+                       "n": n, "m": m, "walks": n * args.wpv, "transitions_per_step": steps_total,
+                       "parallelism": f"walk shards by start-vertex range x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "k_walk (generation)",
+                         "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
+                         "traffic": traffic, "bytes_per_step": bytes_per_step,
+                         "avg_kernel_ms": round(avg_kernel_ms, 3)},
+            "rewalk_latency_10k_batch": rewalk,
+            "cpu_baseline": None,
+        }
+        if world == 1 and args.cpu_baseline != "off":
+            if off is None:
+                off, adj = g.flatten_graph()
+            active = int((deg > 0).sum())
+            line["cpu_baseline"] = cpu_baseline(args, n, active, off, adj, args.cpu_baseline)
+        print(json.dumps(line), flush=True)
+    g.destroy()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

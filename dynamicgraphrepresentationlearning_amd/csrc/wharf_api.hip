@@ -1,0 +1,884 @@
+// C ABI of the WharfMH walk engine (include/wharf_gpu.h): handle management,
+// the graph / batch pipelines (rocPRIM sorts, selects and scans on the
+// handle's stream) and the host side of every entry point.
+#include <cstring>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
+#include <chrono>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "wharf_gpu.h"
+#include "wharf_kernels.h"
+
+using namespace wharf;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct WharfError : std::runtime_error {
+    int code;
+    WharfError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess)                                                                       \
+            throw WharfError(e_ == hipErrorOutOfMemory ? WHARF_E_NOMEM : WHARF_E_HIP,               \
+                             std::string(#x) + ": " + hipGetErrorString(e_) + " (line " +           \
+                             std::to_string(__LINE__) + ")");                                       \
+    } while (0)
+
+#define REQUIRE(cond, code, msg)                        \
+    do {                                                \
+        if (!(cond)) throw WharfError((code), (msg));   \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void ensure(size_t bytes)
+    {
+        if (bytes <= cap && p) return;
+        release();
+        size_t b = std::max<size_t>(bytes, 256);
+        HIPCHK(hipMalloc(&p, b));
+        cap = b;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct NotNoRewalk {
+    const uint8_t* aff;
+    __device__ bool operator()(uint64_t li) const { return aff[li] != kNoRewalk; }
+};
+
+uint32_t bits_for(uint64_t x)   // bits needed to represent values < x
+{
+    uint32_t b = 0;
+    while (b < 64 && (x - 1) >> b) b++;
+    return b;
+}
+
+}  // namespace
+
+struct wharf_handle {
+    int device = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t ev[4] = {};
+    wharf_config cfg{};
+    uint64_t n = 0, m = 0, lo = 0, hi = 0, n_loc = 0, W = 0;
+    uint32_t L = 0, wpv = 0;
+    bool wide = false, anchors = false, has_walks = false;
+    uint32_t epoch = 0;
+    DevBuf off, adj, vrec, anchor, row_epoch, off2, adj2, anchor2;
+    DevBuf walks, aff, rtab, bitmap, counters, errflag;
+    DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, count, pairs, sel;
+    wharf_stats st{};
+    std::string err;
+
+    void sync() { HIPCHK(hipStreamSynchronize(s)); }
+
+    template <class F> void rp(F&& f)   // run a rocPRIM call with the shared temp buffer
+    {
+        size_t bytes = 0;
+        HIPCHK(f((void*)nullptr, bytes));
+        tmp.ensure(bytes);
+        bytes = tmp.cap;
+        HIPCHK(f(tmp.p, bytes));
+    }
+
+    void sort_u64(uint64_t* in, uint64_t* out, uint64_t cnt, uint32_t end_bit)
+    {
+        rp([&](void* t, size_t& b) { return rocprim::radix_sort_keys(t, b, in, out, cnt, 0u, end_bit, s); });
+    }
+
+    // sorted unique keys of `cnt` keys in k1 -> k1 (count returned), self loops dropped if asked
+    uint64_t unique_keys(uint64_t cnt, bool drop_loops, uint32_t end_bit)
+    {
+        if (cnt == 0) return 0;
+        sort_u64(k1.as<uint64_t>(), k2.as<uint64_t>(), cnt, end_bit);
+        flags.ensure(cnt);
+        launch_unique_flags(k2.as<uint64_t>(), cnt, drop_loops, flags.as<uint8_t>(), s);
+        count.ensure(16);
+        uint64_t* in = k2.as<uint64_t>();
+        uint64_t* out = k1.as<uint64_t>();
+        uint8_t* fl = flags.as<uint8_t>();
+        uint64_t* c = count.as<uint64_t>();
+        rp([&](void* t, size_t& b) { return rocprim::select(t, b, in, fl, out, c, (size_t)cnt, s); });
+        uint64_t res = 0;
+        HIPCHK(hipMemcpyAsync(&res, c, 8, hipMemcpyDeviceToHost, s));
+        sync();
+        return res;
+    }
+
+    // CSR (off, adj) from the sorted unique keys in k1
+    void csr_from_keys(uint64_t mm)
+    {
+        off.ensure((n + 1) * 8);
+        adj.ensure(std::max<uint64_t>(mm, 1) * 4);
+        launch_offsets_from_keys(k1.as<uint64_t>(), mm, n, off.as<uint64_t>(), s);
+        launch_low32(k1.as<uint64_t>(), mm, adj.as<uint32_t>(), s);
+        m = mm;
+    }
+
+    void finish_graph()
+    {
+        wide = m >= (1ull << 32);
+        vrec.ensure(std::max<uint64_t>(n, 1) * (wide ? sizeof(VRec64) : sizeof(VRec32)));
+        launch_vrec(off.as<uint64_t>(), n, vrec.p, wide, s);
+        row_epoch.ensure(std::max<uint64_t>(n, 1) * 4);
+        HIPCHK(hipMemsetAsync(row_epoch.p, 0, std::max<uint64_t>(n, 1) * 4, s));
+        if (anchors) {
+            anchor.ensure(std::max<uint64_t>(m, 1) * 4);
+            launch_fill_u32(anchor.as<uint32_t>(), m, kAnchorNone, s);
+        }
+        bitmap.ensure(((n + 31) / 32 + 1) * 4);
+        sync();
+    }
+
+    // the walk matrix is allocated on first use (and re-allocated by set_shard)
+    void ensure_walks()
+    {
+        if (walks.p) return;
+        walks.ensure(std::max<uint64_t>(W * L, 1) * 4);
+        launch_fill_u32(walks.as<uint32_t>(), W * L, kSent, s);
+        aff.ensure(std::max<uint64_t>(W, 1));
+        has_walks = false;
+    }
+
+    WalkArgs walk_args()
+    {
+        ensure_walks();
+        WalkArgs a{};
+        a.vrec = vrec.p;
+        a.adj = adj.as<uint32_t>();
+        a.anchor = anchors ? anchor.as<uint32_t>() : nullptr;
+        a.row_epoch = row_epoch.as<uint32_t>();
+        a.walks = walks.as<uint32_t>();
+        a.rtab = rtab.as<uint64_t>();
+        a.bitmap = bitmap.as<uint32_t>();
+        a.aff = aff.as<uint8_t>();
+        a.counters = counters.as<unsigned long long>();
+        a.n = n; a.n_loc = n_loc; a.lo = lo; a.W = W;
+        a.L = L; a.epoch = epoch;
+        a.key0 = (uint32_t)cfg.seed; a.key1 = (uint32_t)(cfg.seed >> 32);
+        a.inv_p = 1.0f / cfg.paramP;   // node2vec.h:81 `1 / this->paramP` in float
+        a.inv_q = 1.0f / cfg.paramQ;
+        a.model = cfg.model; a.init = cfg.sampler_init; a.det = cfg.deterministic;
+        return a;
+    }
+
+    float elapsed(int a, int b)
+    {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, ev[a], ev[b]));
+        return ms;
+    }
+
+    void read_counters()
+    {
+        unsigned long long c[2];
+        HIPCHK(hipMemcpyAsync(c, counters.p, 16, hipMemcpyDeviceToHost, s));
+        sync();
+        st.steps = c[0];
+        st.accepts = c[1];
+    }
+};
+
+namespace {
+
+void set_err(wharf_handle* h, const std::string& m)
+{
+    g_last_error = m;
+    if (h) h->err = m;
+}
+
+template <class F>
+int guarded(wharf_handle* h, F&& f)
+{
+    try {
+        if (h) HIPCHK(hipSetDevice(h->device));
+        f();
+        return WHARF_OK;
+    } catch (const WharfError& e) {
+        set_err(h, e.what());
+        return e.code;
+    } catch (const std::exception& e) {
+        set_err(h, e.what());
+        return WHARF_E_INVALID;
+    }
+}
+
+void check_config(const wharf_config* c)
+{
+    REQUIRE(c, WHARF_E_INVALID, "config is null");
+    REQUIRE(c->walks_per_vertex >= 1 && c->walks_per_vertex <= 255, WHARF_E_INVALID, "walks_per_vertex must be 1..255");
+    REQUIRE(c->walk_length >= 2 && c->walk_length <= 255, WHARF_E_INVALID, "walk_length must be 2..255 (types::Position is u8)");
+    REQUIRE(c->model == WHARF_DEEPWALK || c->model == WHARF_NODE2VEC, WHARF_E_INVALID, "Unrecognized random walking model");
+    REQUIRE(c->sampler_init >= WHARF_INIT_RANDOM && c->sampler_init <= WHARF_INIT_WEIGHT, WHARF_E_INVALID,
+            "Unrecognized sampler init strategy");
+    REQUIRE(c->model != WHARF_NODE2VEC || (c->paramP > 0 && c->paramQ > 0), WHARF_E_INVALID, "paramP/paramQ must be > 0");
+}
+
+wharf_handle* new_handle(const wharf_config* cfg, uint64_t n, int device)
+{
+    check_config(cfg);
+    REQUIRE(n >= 1 && n < 0xFFFFFFFEull, WHARF_E_INVALID, "n must be in [1, 2^32-2)");
+    REQUIRE(n * (uint64_t)cfg->walks_per_vertex < (1ull << 32), WHARF_E_INVALID,
+            "n * walks_per_vertex must be < 2^32 (types::WalkID is u32)");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    REQUIRE(device >= 0 && device < ndev, WHARF_E_INVALID, "no such HIP device " + std::to_string(device));
+    HIPCHK(hipSetDevice(device));
+    auto* h = new wharf_handle();
+    h->device = device;
+    h->cfg = *cfg;
+    h->n = n;
+    h->L = cfg->walk_length;
+    h->wpv = cfg->walks_per_vertex;
+    h->lo = cfg->shard_lo;
+    h->hi = cfg->shard_hi ? cfg->shard_hi : n;
+    if (h->lo > h->hi || h->hi > n) {
+        delete h;
+        throw WharfError(WHARF_E_INVALID, "shard range must satisfy shard_lo <= shard_hi <= n");
+    }
+    h->n_loc = h->hi - h->lo;
+    h->W = h->n_loc * h->wpv;
+    h->anchors = cfg->model == WHARF_NODE2VEC && !cfg->deterministic;
+    HIPCHK(hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking));
+    for (auto& e : h->ev) HIPCHK(hipEventCreate(&e));
+    // deterministic draw table: Random(r).lrand() for r < wpv (utility.h:157-206)
+    std::vector<uint64_t> t((size_t)h->wpv * h->L);
+    for (uint32_t r = 0; r < h->wpv; r++) {
+        XoroHost x(r);
+        for (uint32_t j = 0; j < h->L; j++) t[(size_t)r * h->L + j] = x.lrand();
+    }
+    h->rtab.ensure(t.size() * 8);
+    HIPCHK(hipMemcpy(h->rtab.p, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+    h->counters.ensure(64);
+    h->errflag.ensure(64);
+    return h;
+}
+
+void free_handle(wharf_handle* h)
+{
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->s) (void)hipStreamSynchronize(h->s);
+    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->anchor, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
+                      &h->aff, &h->rtab, &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags,
+                      &h->chg, &h->cf, &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel})
+        b->release();
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->s) (void)hipStreamDestroy(h->s);
+    delete h;
+}
+
+// keys in h->k1 (cnt of them) -> canonical CSR
+void build_graph_from_keys(wharf_handle* h, uint64_t cnt, bool drop_loops)
+{
+    const uint64_t mm = h->unique_keys(cnt, drop_loops, 32 + std::max<uint32_t>(bits_for(h->n), 1));
+    h->csr_from_keys(mm);
+    h->finish_graph();
+}
+
+void rmat_keys(wharf_handle* h, uint64_t edges_number, uint64_t vertices_number, uint64_t seed, int directed,
+               double a, double b, double c)
+{
+    REQUIRE(vertices_number >= 2, WHARF_E_INVALID, "vertices_number must be >= 2");
+    REQUIRE(a + b + c <= 1.0, WHARF_E_INVALID, "in rMat: a + b + c add to more than 1");
+    REQUIRE(edges_number < (1ull << 32), WHARF_E_INVALID, "edges_number must be < 2^32 (rMat<unsigned int>)");
+    const uint32_t lg = bits_for(vertices_number);   // pbbs::log2_up
+    RmatParams p;
+    p.n = (uint32_t)(1ull << (lg - 1));              // utility.h:78
+    p.a = a; p.ab = a + b; p.abc = a + b + c;
+    p.h = hash32((uint32_t)hash64(0 + seed));        // pbbs::random(seed).ith_rand(0), rmat_util.h:244
+    const uint64_t total = directed ? edges_number : 2 * edges_number;
+    h->k1.ensure(std::max<uint64_t>(total, 1) * 8);
+    h->k2.ensure(std::max<uint64_t>(total, 1) * 8);
+    launch_rmat_keys(p, edges_number, directed, h->k1.as<uint64_t>(), h->s);
+}
+
+int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, uint32_t flags,
+              uint32_t* affected_out, uint64_t* n_affected)
+{
+    return guarded(h, [&] {
+        REQUIRE(h, WHARF_E_INVALID, "null handle");
+        REQUIRE(m == 0 || pairs, WHARF_E_INVALID, "pairs is null");
+        REQUIRE(m < (1ull << 31), WHARF_E_INVALID, "batch too large");
+        auto t0 = std::chrono::steady_clock::now();
+        h->st.affected = 0;
+        h->st.batch_edges = 0;
+        h->st.steps = h->st.accepts = 0;
+        h->st.last_graph_update_ms = h->st.last_walk_update_ms = h->st.last_walk_kernel_ms = 0;
+        if (n_affected) *n_affected = 0;
+        if (m == 0) return;
+        hipStream_t s = h->s;
+        // 1. batch -> device keys, validated, sorted by (src, dst), deduplicated
+        //    (wharfmh.h:450-470, 1056-1104)
+        h->pairs.ensure(m * 8);
+        h->k1.ensure(m * 8);
+        h->k2.ensure(m * 8);
+        HIPCHK(hipMemcpyAsync(h->pairs.p, pairs, m * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(h->errflag.p, 0, 8, s));
+        launch_pairs_to_keys(h->pairs.as<uint32_t>(), m, h->n, h->k1.as<uint64_t>(),
+                             h->errflag.as<unsigned long long>(), s);
+        HIPCHK(hipEventRecord(h->ev[0], s));
+        const uint64_t mb = h->unique_keys(m, (flags & WHARF_REMOVE_DUPS) != 0, 32 + std::max<uint32_t>(bits_for(h->n), 1));
+        unsigned long long errv = 0;
+        HIPCHK(hipMemcpy(&errv, h->errflag.p, 8, hipMemcpyDeviceToHost));
+        REQUIRE(errv == 0, WHARF_E_INVALID, "edge endpoint >= number_of_vertices()");
+        h->st.batch_edges = mb;
+        if (mb == 0) return;
+        uint64_t* bkeys = h->k1.as<uint64_t>();
+
+        // 2. source runs (pack_index, wharfmh.h:475-481)
+        h->flags.ensure(mb);
+        launch_run_flags(bkeys, mb, h->flags.as<uint8_t>(), s);
+        h->runstart.ensure(mb * 4);
+        {
+            auto cnt_it = rocprim::counting_iterator<uint32_t>(0);
+            uint8_t* fl = h->flags.as<uint8_t>();
+            uint32_t* rsp = h->runstart.as<uint32_t>();
+            uint64_t* c = h->count.as<uint64_t>();
+            h->rp([&](void* t, size_t& b) { return rocprim::select(t, b, cnt_it, fl, rsp, c, (size_t)mb, s); });
+        }
+        // 3. which batch edges change their row (uniont / difference), exclusive scan
+        h->chg.ensure((mb + 1) * 4);
+        h->cf.ensure((mb + 1) * 4);
+        HIPCHK(hipMemsetAsync(h->chg.as<uint32_t>() + mb, 0, 4, s));
+        launch_batch_change(bkeys, mb, h->off.as<uint64_t>(), h->adj.as<uint32_t>(), insert, h->chg.as<uint32_t>(), s);
+        {
+            uint32_t* in = h->chg.as<uint32_t>();
+            uint32_t* out = h->cf.as<uint32_t>();
+            h->rp([&](void* t, size_t& b) {
+                return rocprim::exclusive_scan(t, b, in, out, 0u, (size_t)(mb + 1), rocprim::plus<uint32_t>(), s);
+            });
+        }
+        uint64_t k = 0;
+        uint32_t total_chg = 0;
+        HIPCHK(hipMemcpyAsync(&k, h->count.p, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&total_chg, h->cf.as<uint32_t>() + mb, 4, hipMemcpyDeviceToHost, s));
+        h->sync();
+
+        // 4. new CSR: offsets, moved old edges, placed new edges; samplers of
+        //    the batch sources are reset (wharfmh.h:504-540, 652-690)
+        const uint64_t m_new = insert ? h->m + total_chg : h->m - total_chg;
+        h->epoch++;
+        h->runs.ensure(k * sizeof(RunInfo));
+        HIPCHK(hipMemsetAsync(h->bitmap.p, 0, ((h->n + 31) / 32 + 1) * 4, s));
+        launch_run_info(bkeys, h->runstart.as<uint32_t>(), k, mb, h->off.as<uint64_t>(), h->runs.as<RunInfo>(),
+                        h->bitmap.as<uint32_t>(), h->anchors ? h->row_epoch.as<uint32_t>() : nullptr, h->epoch, s);
+        h->off2.ensure((h->n + 1) * 8);
+        h->adj2.ensure(std::max<uint64_t>(m_new, 1) * 4);
+        if (h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 4);
+        launch_new_offsets(h->off.as<uint64_t>(), h->n, bkeys, mb, h->cf.as<uint32_t>(), insert, h->off2.as<uint64_t>(), s);
+        launch_move_edges(h->adj.as<uint32_t>(), h->anchors ? h->anchor.as<uint32_t>() : nullptr, h->m,
+                          h->runs.as<RunInfo>(), k, bkeys, h->cf.as<uint32_t>(), h->off2.as<uint64_t>(), insert,
+                          h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint32_t>() : nullptr, m_new, s);
+        if (insert)
+            launch_place_new(bkeys, mb, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(), h->runstart.as<uint32_t>(), k,
+                             h->runs.as<RunInfo>(), h->adj.as<uint32_t>(), h->off2.as<uint64_t>(),
+                             h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint32_t>() : nullptr, m_new, s);
+        std::swap(h->off, h->off2);
+        std::swap(h->adj, h->adj2);
+        if (h->anchors) std::swap(h->anchor, h->anchor2);
+        h->m = m_new;
+        const bool wide_new = m_new >= (1ull << 32);
+        if (wide_new != h->wide) {
+            h->wide = wide_new;
+            h->vrec.release();
+            h->vrec.ensure(h->n * (h->wide ? sizeof(VRec64) : sizeof(VRec32)));
+        }
+        launch_vrec(h->off.as<uint64_t>(), h->n, h->vrec.p, h->wide, s);
+        HIPCHK(hipEventRecord(h->ev[1], s));
+
+        // 5. rewalk points + suffix re-walk in one pass over the walk matrix
+        //    (wharfmh.h:519-537 and batch_walk_update 733-923)
+        if (h->has_walks && h->W) {
+            HIPCHK(hipMemsetAsync(h->counters.p, 0, 16, s));
+            WalkArgs a = h->walk_args();
+            HIPCHK(hipEventRecord(h->ev[2], s));
+            a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
+            launch_walk(a, h->wide, true, s);
+            HIPCHK(hipEventRecord(h->ev[3], s));
+            // ascending affected walk ids
+            h->sel.ensure(h->W * 8);
+            h->pairs.ensure(h->W * 4);
+            auto cnt_it = rocprim::counting_iterator<uint64_t>(0);
+            uint64_t* out = h->sel.as<uint64_t>();
+            uint64_t* c = h->count.as<uint64_t>();
+            NotNoRewalk pred{h->aff.as<uint8_t>()};
+            h->rp([&](void* t, size_t& b) { return rocprim::select(t, b, cnt_it, out, c, (size_t)h->W, pred, s); });
+            uint64_t naff = 0;
+            HIPCHK(hipMemcpyAsync(&naff, c, 8, hipMemcpyDeviceToHost, s));
+            h->sync();
+            launch_li_to_wid(out, naff, h->n, h->n_loc, h->lo, h->pairs.as<uint32_t>(), s);
+            if (affected_out && naff)
+                HIPCHK(hipMemcpyAsync(affected_out, h->pairs.p, naff * 4, hipMemcpyDeviceToHost, s));
+            h->sync();
+            h->st.affected = naff;
+            if (n_affected) *n_affected = naff;
+            h->read_counters();
+            h->st.last_walk_kernel_ms = h->elapsed(2, 3);
+            h->st.last_walk_update_ms = h->elapsed(1, 3);
+        } else {
+            h->sync();
+        }
+        h->st.last_graph_update_ms = h->elapsed(0, 1);
+        h->st.last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+void wharf_config_default(wharf_config* c)
+{
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    c->walks_per_vertex = 10;              // globals.h:7
+    c->walk_length = 80;                   // globals.h:10
+    c->model = WHARF_DEEPWALK;             // experiments' default (-model deepwalk, throughput-latency.cpp:13)
+    c->paramP = 4.0f;                      // globals.h:16
+    c->paramQ = 1.0f;                      // globals.h:19
+    c->sampler_init = WHARF_INIT_WEIGHT;   // globals.h:22
+    c->deterministic = 1;                  // globals.h:28
+    c->seed = 0x5EED;
+}
+
+const char* wharf_last_error(const wharf_handle* h) { return h ? h->err.c_str() : g_last_error.c_str(); }
+int wharf_abi_version(void) { return WHARF_ABI_VERSION; }
+
+int wharf_device_count(int* count)
+{
+    return guarded(nullptr, [&] {
+        REQUIRE(count, WHARF_E_INVALID, "count is null");
+        HIPCHK(hipGetDeviceCount(count));
+    });
+}
+
+int wharf_create(const wharf_config* cfg, uint64_t n, uint64_t m, const uint64_t* offsets, const uint32_t* targets,
+                 int device, wharf_handle** out)
+{
+    wharf_handle* h = nullptr;
+    int rc = guarded(nullptr, [&] {
+        REQUIRE(out, WHARF_E_INVALID, "out is null");
+        REQUIRE(offsets && (m == 0 || targets), WHARF_E_INVALID, "offsets/targets is null");
+        for (uint64_t v = 0; v < n; v++)
+            REQUIRE(offsets[v] <= (v + 1 < n ? offsets[v + 1] : m), WHARF_E_INVALID, "offsets must be non-decreasing and <= m");
+        h = new_handle(cfg, n, device);
+        std::vector<uint64_t> off(offsets, offsets + n);
+        off.push_back(m);
+        h->off2.ensure((n + 1) * 8);
+        HIPCHK(hipMemcpyAsync(h->off2.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, h->s));
+        h->adj2.ensure(std::max<uint64_t>(m, 1) * 4);
+        if (m) HIPCHK(hipMemcpyAsync(h->adj2.p, targets, m * 4, hipMemcpyHostToDevice, h->s));
+        h->k1.ensure(std::max<uint64_t>(m, 1) * 8);
+        h->k2.ensure(std::max<uint64_t>(m, 1) * 8);
+        HIPCHK(hipMemsetAsync(h->errflag.p, 0, 8, h->s));
+        launch_csr_to_keys(h->off2.as<uint64_t>(), n, h->adj2.as<uint32_t>(), h->k1.as<uint64_t>(),
+                           h->errflag.as<unsigned long long>(), h->s);
+        unsigned long long errv = 0;
+        HIPCHK(hipMemcpyAsync(&errv, h->errflag.p, 8, hipMemcpyDeviceToHost, h->s));
+        h->sync();
+        REQUIRE(errv == 0, WHARF_E_INVALID, "edge target >= n");
+        build_graph_from_keys(h, m, false);
+        h->k1.release();
+        h->k2.release();
+    });
+    if (rc != WHARF_OK) {
+        free_handle(h);
+        return rc;
+    }
+    *out = h;
+    return WHARF_OK;
+}
+
+int wharf_create_empty(const wharf_config* cfg, uint64_t n, int device, wharf_handle** out)
+{
+    static const uint64_t zero = 0;
+    std::vector<uint64_t> off(n, 0);
+    return wharf_create(cfg, n, 0, n ? off.data() : &zero, nullptr, device, out);
+}
+
+int wharf_create_rmat(const wharf_config* cfg, uint64_t n, uint64_t edges_number, uint64_t vertices_number,
+                      uint64_t seed, double a, double b, double c, int device, wharf_handle** out)
+{
+    wharf_handle* h = nullptr;
+    int rc = guarded(nullptr, [&] {
+        REQUIRE(out, WHARF_E_INVALID, "out is null");
+        REQUIRE(vertices_number >= 2, WHARF_E_INVALID, "vertices_number must be >= 2");
+        REQUIRE((1ull << (bits_for(vertices_number) - 1)) <= n, WHARF_E_INVALID, "n smaller than the RMAT vertex range");
+        h = new_handle(cfg, n, device);
+        rmat_keys(h, edges_number, vertices_number, seed, /*directed=*/0, a, b, c);
+        build_graph_from_keys(h, 2 * edges_number, /*drop self loops*/ true);
+        h->k1.release();
+        h->k2.release();
+        h->tmp.release();
+        h->flags.release();
+    });
+    if (rc != WHARF_OK) {
+        free_handle(h);
+        return rc;
+    }
+    *out = h;
+    return WHARF_OK;
+}
+
+int wharf_destroy(wharf_handle* h)
+{
+    free_handle(h);
+    return WHARF_OK;
+}
+
+int wharf_destroy_index(wharf_handle* h)
+{
+    return guarded(h, [&] {
+        REQUIRE(h, WHARF_E_INVALID, "null handle");
+        h->ensure_walks();
+        launch_fill_u32(h->walks.as<uint32_t>(), h->W * h->L, kSent, h->s);
+        h->sync();
+        h->has_walks = false;
+    });
+}
+
+int wharf_generate(wharf_handle* h)
+{
+    return guarded(h, [&] {
+        REQUIRE(h, WHARF_E_INVALID, "null handle");
+        auto t0 = std::chrono::steady_clock::now();
+        HIPCHK(hipMemsetAsync(h->counters.p, 0, 16, h->s));
+        WalkArgs a = h->walk_args();
+        HIPCHK(hipEventRecord(h->ev[0], h->s));
+        launch_walk(a, h->wide, false, h->s);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(h->ev[1], h->s));
+        h->read_counters();
+        h->has_walks = true;
+        h->st.affected = 0;
+        h->st.last_walk_kernel_ms = h->elapsed(0, 1);
+        h->st.last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    });
+}
+
+int wharf_insert_edges(wharf_handle* h, uint64_t m, const uint32_t* pairs, uint32_t flags, uint32_t* affected_out,
+                       uint64_t* n_affected)
+{
+    return do_update(h, true, m, pairs, flags, affected_out, n_affected);
+}
+
+int wharf_delete_edges(wharf_handle* h, uint64_t m, const uint32_t* pairs, uint32_t flags, uint32_t* affected_out,
+                       uint64_t* n_affected)
+{
+    return do_update(h, false, m, pairs, flags, affected_out, n_affected);
+}
+
+int wharf_number_of_vertices(const wharf_handle* h, uint64_t* n)
+{
+    if (!h || !n) return WHARF_E_INVALID;
+    *n = h->n;
+    return WHARF_OK;
+}
+
+int wharf_number_of_edges(const wharf_handle* h, uint64_t* m)
+{
+    if (!h || !m) return WHARF_E_INVALID;
+    *m = h->m;
+    return WHARF_OK;
+}
+
+int wharf_shard(const wharf_handle* h, uint64_t* lo, uint64_t* hi, uint64_t* walks)
+{
+    if (!h) return WHARF_E_INVALID;
+    if (lo) *lo = h->lo;
+    if (hi) *hi = h->hi;
+    if (walks) *walks = h->W;
+    return WHARF_OK;
+}
+
+int wharf_set_shard(wharf_handle* h, uint64_t lo, uint64_t hi)
+{
+    return guarded(h, [&] {
+        REQUIRE(h, WHARF_E_INVALID, "null handle");
+        if (hi == 0) hi = h->n;
+        REQUIRE(lo <= hi && hi <= h->n, WHARF_E_INVALID, "shard range must satisfy lo <= hi <= n");
+        h->sync();
+        h->walks.release();
+        h->aff.release();
+        h->lo = lo;
+        h->hi = hi;
+        h->n_loc = hi - lo;
+        h->W = h->n_loc * h->wpv;
+        h->cfg.shard_lo = lo;
+        h->cfg.shard_hi = hi;
+        h->has_walks = false;
+    });
+}
+
+int wharf_get_graph(wharf_handle* h, uint64_t* offsets_out, uint32_t* targets_out)
+{
+    return guarded(h, [&] {
+        REQUIRE(h && offsets_out && (h->m == 0 || targets_out), WHARF_E_INVALID, "null argument");
+        HIPCHK(hipMemcpyAsync(offsets_out, h->off.p, (h->n + 1) * 8, hipMemcpyDeviceToHost, h->s));
+        if (h->m) HIPCHK(hipMemcpyAsync(targets_out, h->adj.p, h->m * 4, hipMemcpyDeviceToHost, h->s));
+        h->sync();
+    });
+}
+
+static uint64_t local_index(wharf_handle* h, uint64_t wid)
+{
+    const uint64_t r = wid / h->n, v = wid % h->n;
+    REQUIRE(r < h->wpv && v >= h->lo && v < h->hi, WHARF_E_RANGE,
+            "walk " + std::to_string(wid) + " is not owned by this handle");
+    return r * h->n_loc + (v - h->lo);
+}
+
+int wharf_walk(wharf_handle* h, uint64_t wid, uint32_t* out, uint32_t* len)
+{
+    return guarded(h, [&] {
+        REQUIRE(h && out && len, WHARF_E_INVALID, "null argument");
+        const uint64_t li = local_index(h, wid);
+        h->ensure_walks();
+        h->sel.ensure(h->L * 4);
+        launch_gather_walk(h->walks.as<uint32_t>(), h->W, h->L, li, h->sel.as<uint32_t>(), h->s);
+        HIPCHK(hipMemcpyAsync(out, h->sel.p, h->L * 4, hipMemcpyDeviceToHost, h->s));
+        h->sync();
+        uint32_t c = 0;
+        while (c < h->L && out[c] != kSent) c++;
+        *len = c;
+    });
+}
+
+int wharf_walk_string(wharf_handle* h, uint64_t wid, char* buf, size_t cap, size_t* len)
+{
+    std::vector<uint32_t> v(h ? h->L : 1);
+    uint32_t cnt = 0;
+    int rc = wharf_walk(h, wid, v.data(), &cnt);
+    if (rc) return rc;
+    std::string s;
+    for (uint32_t i = 0; i < cnt; i++) { s += std::to_string(v[i]); s += ' '; }   // wharfmh.h:375
+    if (len) *len = s.size();
+    if (buf) {
+        if (cap < s.size() + 1) {
+            set_err(h, "buffer too small");
+            return WHARF_E_INVALID;
+        }
+        std::memcpy(buf, s.c_str(), s.size() + 1);
+    }
+    return WHARF_OK;
+}
+
+int wharf_vertex_at_walk(wharf_handle* h, uint64_t wid, uint32_t position, uint32_t* vertex)
+{
+    return guarded(h, [&] {
+        REQUIRE(h && vertex, WHARF_E_INVALID, "null argument");
+        REQUIRE(position < h->L, WHARF_E_RANGE, "position >= walk_length");
+        const uint64_t li = local_index(h, wid);
+        h->ensure_walks();
+        HIPCHK(hipMemcpyAsync(vertex, h->walks.as<uint32_t>() + (uint64_t)position * h->W + li, 4, hipMemcpyDeviceToHost, h->s));
+        h->sync();
+    });
+}
+
+static void export_walks_impl(wharf_handle* h, uint32_t* dst, int layout, hipMemcpyKind kind)
+{
+    REQUIRE(h && dst, WHARF_E_INVALID, "null argument");
+    REQUIRE(layout == 0 || layout == 1, WHARF_E_INVALID, "layout must be 0 or 1");
+    const uint64_t bytes = h->W * h->L * 4;
+    if (!bytes) return;
+    h->ensure_walks();
+    if (layout == 1) {
+        HIPCHK(hipMemcpyAsync(dst, h->walks.p, bytes, kind, h->s));
+    } else if (kind == hipMemcpyDeviceToDevice) {
+        launch_transpose(h->walks.as<uint32_t>(), h->W, h->L, dst, h->s);
+    } else {
+        h->sel.ensure(bytes);
+        launch_transpose(h->walks.as<uint32_t>(), h->W, h->L, h->sel.as<uint32_t>(), h->s);
+        HIPCHK(hipMemcpyAsync(dst, h->sel.p, bytes, hipMemcpyDeviceToHost, h->s));
+    }
+    h->sync();
+}
+
+int wharf_export_walks(wharf_handle* h, uint32_t* dst, int layout)
+{
+    return guarded(h, [&] { export_walks_impl(h, dst, layout, hipMemcpyDeviceToHost); });
+}
+
+int wharf_export_walks_device(wharf_handle* h, uint32_t* dst, int layout)
+{
+    return guarded(h, [&] { export_walks_impl(h, dst, layout, hipMemcpyDeviceToDevice); });
+}
+
+int wharf_walk_ids(wharf_handle* h, uint32_t* ids)
+{
+    return guarded(h, [&] {
+        REQUIRE(h && ids, WHARF_E_INVALID, "null argument");
+        for (uint64_t li = 0; li < h->W; li++) {
+            const uint64_t r = li / h->n_loc;
+            ids[li] = (uint32_t)(r * h->n + h->lo + (li - r * h->n_loc));
+        }
+    });
+}
+
+namespace {
+// Builds the inverted index of this handle's walks, sorted by (vertex, key);
+// returns the entry count.  Leaves sort keys in k1 and values in k2.
+uint64_t build_index(wharf_handle* h, int& kb)
+{
+    const uint64_t W = h->W;
+    h->ensure_walks();
+    kb = (int)std::max<uint32_t>(bits_for(h->n * h->wpv * h->L), 1);
+    const int vb = (int)std::max<uint32_t>(bits_for(h->n), 1);
+    REQUIRE(kb + vb <= 64, WHARF_E_INVALID, "index key does not fit 64 bits");
+    h->sel.ensure((W + 1) * 8);
+    h->count.ensure((W + 1) * 8);
+    uint64_t* len = h->sel.as<uint64_t>();
+    uint64_t* base = h->count.as<uint64_t>();
+    HIPCHK(hipMemsetAsync(len + W, 0, 8, h->s));
+    launch_walk_lengths(h->walks.as<uint32_t>(), W, h->L, len, h->s);
+    h->rp([&](void* t, size_t& b) {
+        return rocprim::exclusive_scan(t, b, len, base, (uint64_t)0, (size_t)(W + 1), rocprim::plus<uint64_t>(), h->s);
+    });
+    uint64_t E = 0;
+    HIPCHK(hipMemcpyAsync(&E, base + W, 8, hipMemcpyDeviceToHost, h->s));
+    h->sync();
+    if (!E) return 0;
+    h->k1.ensure(E * 8);
+    h->k2.ensure(E * 8);
+    h->flags.ensure(E * 4);
+    h->pairs.ensure(E * 4);
+    launch_index_entries(h->walks.as<uint32_t>(), W, h->L, h->n, h->n_loc, h->lo, kb, base, h->k1.as<uint64_t>(),
+                         h->flags.as<uint32_t>(), h->s);
+    uint64_t* ki = h->k1.as<uint64_t>();
+    uint64_t* ko = h->k2.as<uint64_t>();
+    uint32_t* vi = h->flags.as<uint32_t>();
+    uint32_t* vo = h->pairs.as<uint32_t>();
+    const unsigned eb = (unsigned)(kb + vb);
+    h->rp([&](void* t, size_t& b) { return rocprim::radix_sort_pairs(t, b, ki, ko, vi, vo, (size_t)E, 0u, eb, h->s); });
+    return E;
+}
+}  // namespace
+
+int wharf_index_size(wharf_handle* h, uint64_t* size)
+{
+    return guarded(h, [&] {
+        REQUIRE(h && size, WHARF_E_INVALID, "null argument");
+        h->ensure_walks();
+        h->sel.ensure((h->W + 1) * 8);
+        h->count.ensure((h->W + 1) * 8);
+        uint64_t* len = h->sel.as<uint64_t>();
+        uint64_t* base = h->count.as<uint64_t>();
+        HIPCHK(hipMemsetAsync(len + h->W, 0, 8, h->s));
+        launch_walk_lengths(h->walks.as<uint32_t>(), h->W, h->L, len, h->s);
+        h->rp([&](void* t, size_t& b) {
+            return rocprim::exclusive_scan(t, b, len, base, (uint64_t)0, (size_t)(h->W + 1), rocprim::plus<uint64_t>(), h->s);
+        });
+        HIPCHK(hipMemcpyAsync(size, base + h->W, 8, hipMemcpyDeviceToHost, h->s));
+        h->sync();
+    });
+}
+
+int wharf_export_index(wharf_handle* h, uint64_t* counts, uint64_t* keys, uint32_t* nexts)
+{
+    return guarded(h, [&] {
+        REQUIRE(h && counts, WHARF_E_INVALID, "null argument");
+        int kb = 0;
+        const uint64_t E = build_index(h, kb);
+        h->runs.ensure(h->n * 8);
+        HIPCHK(hipMemsetAsync(h->runs.p, 0, h->n * 8, h->s));
+        if (E) {
+            REQUIRE(keys && nexts, WHARF_E_INVALID, "null argument");
+            // k2 holds sorted (vertex<<kb | key); split into counts and keys (reuse k1)
+            launch_index_split(h->k2.as<uint64_t>(), E, kb, h->runs.as<unsigned long long>(), h->k1.as<uint64_t>(), h->s);
+            HIPCHK(hipMemcpyAsync(keys, h->k1.p, E * 8, hipMemcpyDeviceToHost, h->s));
+            HIPCHK(hipMemcpyAsync(nexts, h->pairs.p, E * 4, hipMemcpyDeviceToHost, h->s));
+        }
+        HIPCHK(hipMemcpyAsync(counts, h->runs.p, h->n * 8, hipMemcpyDeviceToHost, h->s));
+        h->sync();
+    });
+}
+
+int wharf_get_stats(const wharf_handle* h, wharf_stats* out)
+{
+    if (!h || !out) return WHARF_E_INVALID;
+    *out = h->st;
+    out->n = h->n;
+    out->m = h->m;
+    out->walks = h->W;
+    out->hbm_bytes_walks = h->W * h->L * 4;
+    out->hbm_bytes_graph = (h->n + 1) * 8 + h->m * 4 + h->n * (h->wide ? 16 : 8) + (h->anchors ? h->m * 4 : 0);
+    return WHARF_OK;
+}
+
+int wharf_generate_batch_of_edges(int device, uint64_t edges_number, uint64_t vertices_number, uint64_t batch_seed,
+                                  int self_loops, int directed, double a, double b, double c, uint32_t* out_pairs,
+                                  uint64_t* count)
+{
+    wharf_config cfg;
+    wharf_config_default(&cfg);
+    wharf_handle* h = nullptr;
+    int rc = guarded(nullptr, [&] {
+        REQUIRE(out_pairs && count, WHARF_E_INVALID, "null argument");
+        // a scratch handle on a single vertex (no walks) to own the stream and buffers
+        cfg.walks_per_vertex = 1;
+        cfg.walk_length = 2;
+        h = new_handle(&cfg, 1, device);
+        rmat_keys(h, edges_number, vertices_number, batch_seed, directed, a, b, c);
+        const uint64_t total = directed ? edges_number : 2 * edges_number;
+        const uint32_t nb = bits_for(vertices_number);
+        const uint64_t k = h->unique_keys(total, !self_loops, 32 + std::max<uint32_t>(nb, 1));
+        std::vector<uint64_t> keys(k);
+        if (k) HIPCHK(hipMemcpy(keys.data(), h->k1.p, k * 8, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < k; i++) {
+            out_pairs[2 * i] = (uint32_t)(keys[i] >> 32);
+            out_pairs[2 * i + 1] = (uint32_t)keys[i];
+        }
+        *count = k;
+    });
+    free_handle(h);
+    return rc;
+}
+
+int wharf_szudzik64(int device, int op, uint64_t count, uint64_t* x, uint64_t* y, uint64_t* z)
+{
+    return guarded(nullptr, [&] {
+        REQUIRE(x && y && z && (op == 0 || op == 1), WHARF_E_INVALID, "bad argument");
+        HIPCHK(hipSetDevice(device));
+        if (!count) return;
+        uint64_t* d = nullptr;
+        HIPCHK(hipMalloc(&d, count * 24));
+        try {
+            HIPCHK(hipMemcpy(d, x, count * 8, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(d + count, y, count * 8, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(d + 2 * count, z, count * 8, hipMemcpyHostToDevice));
+            launch_szudzik64(op, count, d, d + count, d + 2 * count, 0);
+            HIPCHK(hipDeviceSynchronize());
+            HIPCHK(hipMemcpy(x, d, count * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(y, d + count, count * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(z, d + 2 * count, count * 8, hipMemcpyDeviceToHost));
+        } catch (...) {
+            (void)hipFree(d);
+            throw;
+        }
+        HIPCHK(hipFree(d));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,151 @@
+// Device-side building blocks of the WharfMH walk engine (gfx950 / CDNA4).
+//
+//   - xoroshiro128+ with the reference's arithmetic-shift seeding
+//     (utils/utility.h:152-223) — host side, used to fill the per-round draw
+//     table of deterministic mode;
+//   - Philox4x32-10 counter-based RNG for MH mode (one independent stream per
+//     (walk, position, epoch), no shared state: replaces the racy global
+//     config::random of metropolis_hastings_sampler.h:121 / deepwalk.h:82);
+//   - the reference's RMAT edge recursion (rmat_util.h:250-271) and pbbs hashes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wharf {
+
+constexpr uint32_t kSent = 0xFFFFFFFEu;        // wharfmh.h:282 (uint32 max - 1)
+constexpr uint32_t kAnchorNone = 0xFFFFFFFFu;  // MH anchor slot not initialised yet
+constexpr uint32_t kNoRewalk = 0xFFu;          // rewalk position "none"
+
+// Philox counter word 3 = (epoch << 4) | stream
+enum : uint32_t { kStreamStep = 0, kStreamAnchor = 1, kStreamBurnin = 2, kStreamPrev = 3 };
+
+// CSR vertex record: one aligned load gives a row's start and length.
+struct VRec32 { uint32_t off, deg; };                 // m < 2^32
+struct alignas(16) VRec64 { uint64_t off, deg; };     // m >= 2^32
+
+template <class VR> __device__ __forceinline__ VR load_vrec(const VR* p, uint32_t v) { return p[v]; }
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Random123); 10 rounds, key bumped between rounds.
+// ---------------------------------------------------------------------------
+struct P4 { uint32_t x0, x1, x2, x3; };
+
+__device__ __forceinline__ P4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1)
+{
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    return P4{c0, c1, c2, c3};
+}
+
+// uniform index in [0, deg): multiply-high (Lemire, no rejection)
+__device__ __forceinline__ uint64_t pick32(uint32_t r, uint32_t deg) { return __umulhi(r, deg); }
+__device__ __forceinline__ uint64_t pick64(uint32_t r, uint64_t deg)
+{
+    // (r * deg) >> 32 for deg up to 2^64 with a 64x32 -> 96-bit product
+    const uint64_t lo = (uint64_t)r * (uint32_t)deg;
+    const uint64_t hi = (uint64_t)r * (uint32_t)(deg >> 32);
+    return hi + (lo >> 32);
+}
+
+// drand-like uniform in [0,1) from 53 bits
+__device__ __forceinline__ double u01(uint32_t hi, uint32_t lo)
+{
+    return (double)((((uint64_t)hi << 32) | lo) >> 11) * 0x1.0p-53;
+}
+
+// x % d for a 64-bit x and 32-bit d (utility.h:220 irand: lrand() % max)
+__device__ __forceinline__ uint32_t umod64_32(uint64_t x, uint32_t d) { return (uint32_t)(x % (uint64_t)d); }
+
+// ---------------------------------------------------------------------------
+// pbbs hashes (pbbslib/utilities.h:108-146) and the RMAT recursion
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t hash32(uint32_t a)
+{
+    a = (a + 0x7ed55d16u) + (a << 12);
+    a = (a ^ 0xc761c23cu) ^ (a >> 19);
+    a = (a + 0x165667b1u) + (a << 5);
+    a = (a + 0xd3a2646cu) ^ (a << 9);
+    a = (a + 0xfd7046c5u) + (a << 3);
+    a = (a ^ 0xb55a4f09u) ^ (a >> 16);
+    return a;
+}
+
+__host__ __device__ __forceinline__ uint64_t hash64(uint64_t u)
+{
+    uint64_t v = u * 3935559000370003845ull + 2691343689449507681ull;
+    v ^= v >> 21;
+    v ^= v << 37;
+    v ^= v >> 4;
+    v *= 4768777513237032717ull;
+    v ^= v << 20;
+    v ^= v >> 41;
+    v ^= v << 5;
+    return v;
+}
+
+struct RmatParams { double a, ab, abc; uint32_t n, h; };
+
+// rMat<unsigned int>::operator() (rmat_util.h:255-271): level t of the
+// recursion (quadrant size n >> (t+1)) reads hashDouble(randStart + t*randStride).
+__device__ __forceinline__ void rmat_edge(const RmatParams& p, uint32_t i, uint32_t& src, uint32_t& dst)
+{
+    const uint32_t start = hash32((uint32_t)(2u * i) * p.h);
+    const uint32_t stride = hash32((uint32_t)(2u * i + 1u) * p.h);
+    uint32_t x = 0, y = 0, nn = p.n, t = 0;
+    while (nn > 1) {
+        const double d = (double)hash32(start + t * stride) / 4294967295.0;
+        const uint32_t half = nn >> 1;
+        if (d < p.a) {
+        } else if (d < p.ab) {
+            y += half;
+        } else if (d < p.abc) {
+            x += half;
+        } else {
+            x += half;
+            y += half;
+        }
+        nn = half;
+        t++;
+    }
+    src = x;
+    dst = y;
+}
+
+// ---------------------------------------------------------------------------
+// host: utility::Random (utils/utility.h:157-206).  The seed word is a signed
+// long long, so the splitmix shifts are arithmetic.
+// ---------------------------------------------------------------------------
+struct XoroHost {
+    uint64_t s0, s1;
+    explicit XoroHost(uint64_t seed)
+    {
+        for (int i = 0; i < 2; i++) {
+            seed += 0x9E3779B97F4A7C15ull;
+            int64_t z = (int64_t)seed;
+            z = (int64_t)((uint64_t)(z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull);
+            z = (int64_t)((uint64_t)(z ^ (z >> 27)) * 0x94D049BB133111EBull);
+            (i == 0 ? s0 : s1) = (uint64_t)(z ^ (z >> 31));
+        }
+    }
+    uint64_t lrand()
+    {
+        const uint64_t a = s0;
+        uint64_t b = s1;
+        const uint64_t r = a + b;
+        b ^= a;
+        s0 = ((a << 55) | (a >> 9)) ^ b ^ (b << 14);
+        s1 = (b << 36) | (b >> 28);
+        return r;
+    }
+};
+
+}  // namespace wharf

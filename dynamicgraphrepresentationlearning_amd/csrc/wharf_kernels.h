@@ -1,0 +1,75 @@
+// Kernel-side interface of the WharfMH walk engine (shared by the kernels and
+// the C-ABI implementation).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "wharf_device.h"
+
+namespace wharf {
+
+enum { kDeepWalk = 0, kNode2Vec = 1 };
+enum { kInitRandom = 0, kInitBurnin = 1, kInitWeight = 2 };
+
+struct WalkArgs {
+    const void* vrec;            // VRec32[n] or VRec64[n]
+    const uint32_t* adj;         // CSR targets
+    uint32_t* anchor;            // MH anchors per CSR slot (node2vec MH), else null
+    const uint32_t* row_epoch;   // epoch of each row's last sampler reset (MH)
+    uint32_t* walks;             // [L][W]
+    const uint64_t* rtab;        // deterministic draws [wpv][L]
+    const uint32_t* bitmap;      // batch sources (re-walk)
+    uint8_t* aff;                // per owned walk: re-walk position or kNoRewalk
+    unsigned long long* counters;  // [0] steps, [1] accepts
+    uint64_t n, n_loc, lo, W;
+    uint32_t L, epoch;
+    uint32_t key0, key1;
+    float inv_p, inv_q;
+    int model, init, det;
+    int scan_only;               // re-walk: only find rewalk points (apply_walk_updates=false)
+};
+
+struct RunInfo {
+    uint64_t off, end;   // old row [off, end)
+    uint32_t src, rs, re, pad;
+};
+
+unsigned grid_for(uint64_t work, unsigned block);
+
+void launch_walk(const WalkArgs& a, bool wide, bool rewalk, hipStream_t s);
+void launch_vrec(const uint64_t* off, uint64_t n, void* vrec, bool wide, hipStream_t s);
+void launch_rmat_keys(const RmatParams& p, uint64_t M, int directed, uint64_t* keys, hipStream_t s);
+void launch_pairs_to_keys(const uint32_t* pairs, uint64_t m, uint64_t n, uint64_t* keys, unsigned long long* err, hipStream_t s);
+void launch_csr_to_keys(const uint64_t* off, uint64_t n, const uint32_t* tgt, uint64_t* keys, unsigned long long* err, hipStream_t s);
+void launch_unique_flags(const uint64_t* keys, uint64_t m, int drop_loops, uint8_t* keep, hipStream_t s);
+void launch_offsets_from_keys(const uint64_t* keys, uint64_t m, uint64_t n, uint64_t* off, hipStream_t s);
+void launch_low32(const uint64_t* keys, uint64_t m, uint32_t* out, hipStream_t s);
+void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off, const uint32_t* adj, int insert,
+                         uint32_t* chg, hipStream_t s);
+void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_t s);
+void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
+                     RunInfo* runs, uint32_t* bitmap, uint32_t* row_epoch, uint32_t epoch, hipStream_t s);
+void launch_new_offsets(const uint64_t* off, uint64_t n, const uint64_t* bkeys, uint64_t mb, const uint32_t* cf,
+                        int insert, uint64_t* noff, hipStream_t s);
+void launch_move_edges(const uint32_t* adj, const uint32_t* anc, uint64_t m, const RunInfo* runs, uint64_t k,
+                       const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
+                       uint32_t* nanc, uint64_t cap, hipStream_t s);
+void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf,
+                      const uint32_t* run_start, uint64_t k, const RunInfo* runs, const uint32_t* adj,
+                      const uint64_t* noff, uint32_t* nadj, uint32_t* nanc, uint64_t cap, hipStream_t s);
+void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s);
+void launch_gather_walk(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* out, hipStream_t s);
+void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t* len, hipStream_t s);
+void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc, uint64_t lo,
+                          int kb, const uint64_t* col_base, uint64_t* skeys, uint32_t* vals, hipStream_t s);
+void launch_index_split(const uint64_t* skeys, uint64_t E, int kb, unsigned long long* counts, uint64_t* keys,
+                        hipStream_t s);
+void launch_li_to_wid(const uint64_t* li, uint64_t cnt, uint64_t n, uint64_t n_loc, uint64_t lo, uint32_t* out,
+                      hipStream_t s);
+void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s);
+void launch_szudzik64(int op, uint64_t cnt, uint64_t* x, uint64_t* y, uint64_t* z, hipStream_t s);
+
+}  // namespace wharf

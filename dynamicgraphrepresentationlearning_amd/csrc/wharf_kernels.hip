@@ -1,0 +1,606 @@
+// HIP kernels of the WharfMH walk engine, written for gfx950 (CDNA4).
+//
+// Layout in HBM:
+//   vrec[n]        {row offset, degree}: one aligned 8-B (16-B when m >= 2^32) load per step
+//   adj[m]         u32 targets, rows ascending (the order CompressedEdges::get_edges yields)
+//   walks[L][W]    position-major walk matrix: lane i of a wave owns walk i, so every
+//                  store/load of one position by a wave is one contiguous 256-B segment
+//   anchor[m]      frozen MH anchor per (cur, slot of prev in adj(cur)) (node2vec MH)
+//   bitmap[n/32]   batch-source set for the rewalk-point scan
+#include "wharf_kernels.h"
+
+namespace wharf {
+
+// ---------------------------------------------------------------------------
+// wave-level sum + one atomic per wave for the step / acceptance counters
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wave_add(unsigned long long* dst, uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, (unsigned long long)v);
+}
+
+template <class VR>
+__device__ __forceinline__ bool row_contains(const uint32_t* __restrict__ adj, const VR& r, uint32_t x)
+{
+    // std::binary_search over the ascending row (node2vec.h:112-119)
+    uint64_t lo = r.off, hi = r.off + r.deg;
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (adj[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return lo < r.off + r.deg && adj[lo] == x;
+}
+
+template <class VR>
+__device__ __forceinline__ int64_t row_find(const uint32_t* __restrict__ adj, const VR& r, uint32_t x)
+{
+    uint64_t lo = r.off, hi = r.off + r.deg;
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (adj[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return (lo < r.off + r.deg && adj[lo] == x) ? (int64_t)lo : -1;
+}
+
+template <class VR>
+__device__ __forceinline__ uint64_t pick(uint32_t r, const VR& rec)
+{
+    if constexpr (sizeof(VR) == 8) return pick32(r, (uint32_t)rec.deg);
+    else return pick64(r, rec.deg);
+}
+
+// node2vec.h:74-88 (DeepWalk: deepwalk.h:67-70 returns 1)
+template <int MODEL, class VR>
+__device__ __forceinline__ float weight(const WalkArgs& a, uint32_t prev, const VR& rprev, uint32_t c)
+{
+    if constexpr (MODEL == kDeepWalk) return 1.0f;
+    if (c == prev) return a.inv_p;
+    if (row_contains(a.adj, rprev, c)) return 1.0f;
+    return a.inv_q;
+}
+
+// MetropolisHastingsSampler::init (metropolis_hastings_sampler.h:69-108) with
+// proposals from the (cur, prev, row_epoch[cur]) Philox stream.
+template <class VR>
+__device__ uint32_t anchor_init(const WalkArgs& a, uint32_t cur, const VR& rcur, uint32_t prev, const VR& rprev)
+{
+    const uint32_t ep = a.row_epoch[cur] << 4;
+    P4 r = philox4x32_10(cur, prev, 0, ep | kStreamAnchor, a.key0, a.key1);
+    uint32_t last = a.adj[rcur.off + pick(r.x0, rcur)];
+    if (a.init == kInitWeight) {
+        float best = weight<kNode2Vec>(a, prev, rprev, last);
+        for (uint32_t j = 1; j <= 20; j++) {
+            r = philox4x32_10(cur, prev, j, ep | kStreamAnchor, a.key0, a.key1);
+            const uint32_t cand = a.adj[rcur.off + pick(r.x0, rcur)];
+            const float w = weight<kNode2Vec>(a, prev, rprev, cand);
+            if (w > best) { best = w; last = cand; }
+        }
+    } else if (a.init == kInitBurnin) {
+        for (uint32_t i = 0; i < 100; i++) {
+            r = philox4x32_10(cur, prev, i, ep | kStreamBurnin, a.key0, a.key1);
+            const uint32_t cand = a.adj[rcur.off + pick(r.x0, rcur)];
+            const float wn = weight<kNode2Vec>(a, prev, rprev, cand);
+            const float wl = weight<kNode2Vec>(a, prev, rprev, last);
+            if (wl < wn || u01(r.x1, r.x2) <= (double)wn / (double)wl) last = cand;
+        }
+    }
+    return last;
+}
+
+// SamplerManager::find (copy, so the anchor stays frozen: libcuckoo find()
+// returns by value, cuckoohash_map.hh:596-609).  Lazily initialised; every
+// writer of a slot writes the same value (pure function of the slot's inputs).
+template <class VR>
+__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, uint32_t cur, const VR& rcur, uint32_t prev,
+                                               const VR& rprev)
+{
+    const int64_t slot = row_find(a.adj, rcur, prev);
+    if (slot < 0) return anchor_init(a, cur, rcur, prev, rprev);
+    uint32_t an = a.anchor[slot];
+    if (an == kAnchorNone) {
+        an = anchor_init(a, cur, rcur, prev, rprev);
+        a.anchor[slot] = an;
+    }
+    return an;
+}
+
+// ---------------------------------------------------------------------------
+// The walk kernel: generation (REWALK=false, wharfmh.h:275-326) and fused
+// rewalk-point scan + suffix re-walk (REWALK=true, wharfmh.h:519-537 + 761-859).
+// One lane per walk; lane li owns walk matrix column li.
+// ---------------------------------------------------------------------------
+template <class VR, int MODEL, bool DET, bool REWALK>
+__global__ __launch_bounds__(256) void k_walk(WalkArgs a)
+{
+    const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t steps = 0, accepts = 0;
+    if (li < a.W) {
+        const VR* __restrict__ vrec = reinterpret_cast<const VR*>(a.vrec);
+        const uint32_t* __restrict__ adj = a.adj;
+        uint32_t* __restrict__ walks = a.walks;
+        const uint64_t W = a.W;
+        const uint64_t r = li / a.n_loc;
+        const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
+        const uint64_t wid = r * a.n + v;
+
+        uint32_t p = 0, cur = v, prev = v;
+        bool go = true;
+        if constexpr (REWALK) {
+            // min position of any batch source in this walk, over the old corpus
+            p = kNoRewalk;
+            for (uint32_t pos = 0; pos < a.L; pos++) {
+                const uint32_t x = walks[(uint64_t)pos * W + li];
+                if (x == kSent) break;
+                if ((a.bitmap[x >> 5] >> (x & 31)) & 1u) { p = pos; cur = x; break; }
+            }
+            a.aff[li] = (uint8_t)p;
+            go = p != kNoRewalk && !a.scan_only;
+            if (go && MODEL == kNode2Vec && !DET && p > 0) prev = walks[(uint64_t)(p - 1) * W + li];
+        } else {
+            walks[li] = v;
+        }
+        if (go) {
+            const uint32_t ep = a.epoch << 4;
+            const uint32_t wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
+            if constexpr (MODEL == kNode2Vec && !DET) {
+                if (p == 0) {
+                    // Node2Vec::initial_state: prev = random neighbour (node2vec.h:42-50)
+                    const VR rv = vrec[cur];
+                    if (rv.deg) {
+                        const P4 q = philox4x32_10(wlo, whi, 0, ep | kStreamPrev, a.key0, a.key1);
+                        prev = adj[rv.off + pick(q.x0, rv)];
+                    }
+                }
+            }
+            const uint64_t* __restrict__ rt = DET ? a.rtab + r * a.L : nullptr;
+            uint32_t pos = p;
+            for (; pos + 1 < a.L; pos++) {
+                const VR rc = vrec[cur];
+                if (rc.deg == 0) break;   // dead end: the walk stops (reference: lrand() % 0)
+                uint32_t nxt;
+                if constexpr (DET) {
+                    // Random(wid / n) restarted at the walk's first re-walked position
+                    const uint64_t x = rt[pos - p];
+                    if constexpr (sizeof(VR) == 8) nxt = adj[rc.off + umod64_32(x, (uint32_t)rc.deg)];
+                    else nxt = adj[rc.off + x % rc.deg];
+                } else {
+                    const P4 q = philox4x32_10(wlo, whi, pos, ep | kStreamStep, a.key0, a.key1);
+                    const uint32_t c = adj[rc.off + pick(q.x0, rc)];
+                    if constexpr (MODEL == kDeepWalk) {
+                        nxt = c;   // weights are all 1: sample() always accepts
+                        accepts++;
+                    } else {
+                        const VR rp = vrec[prev];
+                        const uint32_t an = anchor_get(a, cur, rc, prev, rp);
+                        const float wc = weight<MODEL>(a, prev, rp, c);
+                        const float wa = (an == c) ? wc : weight<MODEL>(a, prev, rp, an);
+                        const bool ok = (wa < wc) || (u01(q.x1, q.x2) <= (double)wc / (double)wa);
+                        nxt = ok ? c : an;
+                        accepts += ok;
+                    }
+                }
+                walks[(uint64_t)(pos + 1) * W + li] = nxt;
+                steps++;
+                prev = cur;
+                cur = nxt;
+            }
+            for (pos = pos + 1; pos < a.L; pos++) walks[(uint64_t)pos * W + li] = kSent;
+        }
+    }
+    wave_add(a.counters + 0, steps);
+    wave_add(a.counters + 1, accepts);
+}
+
+template <class VR>
+static void launch_walk_vr(const WalkArgs& a, bool rewalk, hipStream_t s)
+{
+    const dim3 grid((unsigned)((a.W + 255) / 256)), block(256);
+    const bool det = a.det != 0;
+    const int model = a.model;
+#define WHARF_LAUNCH(M, D, R) hipLaunchKernelGGL((k_walk<VR, M, D, R>), grid, block, 0, s, a)
+    if (det) {
+        if (rewalk) WHARF_LAUNCH(kDeepWalk, true, true); else WHARF_LAUNCH(kDeepWalk, true, false);
+    } else if (model == kDeepWalk) {
+        if (rewalk) WHARF_LAUNCH(kDeepWalk, false, true); else WHARF_LAUNCH(kDeepWalk, false, false);
+    } else {
+        if (rewalk) WHARF_LAUNCH(kNode2Vec, false, true); else WHARF_LAUNCH(kNode2Vec, false, false);
+    }
+#undef WHARF_LAUNCH
+}
+
+void launch_walk(const WalkArgs& a, bool wide, bool rewalk, hipStream_t s)
+{
+    if (a.W == 0) return;
+    if (wide) launch_walk_vr<VRec64>(a, rewalk, s);
+    else launch_walk_vr<VRec32>(a, rewalk, s);
+}
+
+// ---------------------------------------------------------------------------
+// graph construction / maintenance
+// ---------------------------------------------------------------------------
+__global__ void k_rmat_keys(RmatParams p, uint64_t M, int directed, uint64_t* __restrict__ keys)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t s, d;
+        rmat_edge(p, (uint32_t)i, s, d);
+        keys[i] = ((uint64_t)s << 32) | d;
+        if (!directed) keys[M + i] = ((uint64_t)d << 32) | s;
+    }
+}
+
+__global__ void k_pairs_to_keys(const uint32_t* __restrict__ pairs, uint64_t m, uint64_t n,
+                                uint64_t* __restrict__ keys, unsigned long long* __restrict__ err)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = pairs[2 * i], d = pairs[2 * i + 1];
+        if (s >= n || d >= n) atomicOr(err, 1ull);
+        keys[i] = ((uint64_t)s << 32) | d;
+    }
+}
+
+__global__ void k_csr_to_keys(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ tgt,
+                              uint64_t* __restrict__ keys, unsigned long long* __restrict__ err)
+{
+    // one block per 64 rows: lanes sweep a row's targets contiguously
+    const uint64_t v0 = (uint64_t)blockIdx.x * 64;
+    for (uint64_t v = v0 + threadIdx.x / 64; v < min(v0 + 64, n); v += blockDim.x / 64) {
+        const uint64_t b = off[v], e = off[v + 1];
+        for (uint64_t j = b + (threadIdx.x & 63); j < e; j += 64) {
+            const uint32_t d = tgt[j];
+            if (d >= n) atomicOr(err, 1ull);
+            keys[j] = (v << 32) | d;
+        }
+    }
+}
+
+// keep[i]: first of its run of equal keys, and not a self loop when asked
+__global__ void k_unique_flags(const uint64_t* __restrict__ keys, uint64_t m, int drop_loops, uint8_t* __restrict__ keep)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        bool ok = i == 0 || keys[i - 1] != k;
+        if (drop_loops && (uint32_t)(k >> 32) == (uint32_t)k) ok = false;
+        keep[i] = ok;
+    }
+}
+
+// off[v] = lower_bound(keys, v << 32) for v in [0, n]
+__global__ void k_offsets_from_keys(const uint64_t* __restrict__ keys, uint64_t m, uint64_t n, uint64_t* __restrict__ off)
+{
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = v << 32;
+        uint64_t lo = 0, hi = m;
+        while (lo < hi) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            if (keys[mid] < t) lo = mid + 1; else hi = mid;
+        }
+        off[v] = lo;
+    }
+}
+
+__global__ void k_low32(const uint64_t* __restrict__ keys, uint64_t m, uint32_t* __restrict__ out)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = (uint32_t)keys[i];
+}
+
+template <class VR>
+__global__ void k_vrec(const uint64_t* __restrict__ off, uint64_t n, VR* __restrict__ vrec)
+{
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        VR r;
+        r.off = (decltype(r.off))off[v];
+        r.deg = (decltype(r.deg))(off[v + 1] - off[v]);
+        vrec[v] = r;
+    }
+}
+
+void launch_vrec(const uint64_t* off, uint64_t n, void* vrec, bool wide, hipStream_t s)
+{
+    const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256 + 1, 65535);
+    if (wide) hipLaunchKernelGGL(k_vrec<VRec64>, g, 256, 0, s, off, n, (VRec64*)vrec);
+    else hipLaunchKernelGGL(k_vrec<VRec32>, g, 256, 0, s, off, n, (VRec32*)vrec);
+}
+
+// Per batch edge (sorted, unique): does it change its source row?
+//   insert: dst not yet in adj(src)  (tree_plus::uniont, wharfmh.h:511)
+//   delete: dst present in adj(src)  (tree_plus::difference, wharfmh.h:659)
+__global__ void k_batch_change(const uint64_t* __restrict__ bkeys, uint64_t mb, const uint64_t* __restrict__ off,
+                               const uint32_t* __restrict__ adj, int insert, uint32_t* __restrict__ chg)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mb; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = (uint32_t)(bkeys[i] >> 32), d = (uint32_t)bkeys[i];
+        uint64_t lo = off[s], hi = off[s + 1];
+        const uint64_t end = hi;
+        while (lo < hi) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            if (adj[mid] < d) lo = mid + 1; else hi = mid;
+        }
+        const bool present = lo < end && adj[lo] == d;
+        chg[i] = insert ? !present : present;
+    }
+}
+
+// run starts of equal sources -> flag
+__global__ void k_run_flags(const uint64_t* __restrict__ bkeys, uint64_t mb, uint8_t* __restrict__ f)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mb; i += (uint64_t)gridDim.x * blockDim.x)
+        f[i] = i == 0 || (bkeys[i] >> 32) != (bkeys[i - 1] >> 32);
+}
+
+// per source run j: src, old row [off, end), batch run [rs, re)
+__global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ run_start, uint64_t k,
+                           uint64_t mb, const uint64_t* __restrict__ off, RunInfo* __restrict__ runs,
+                           uint32_t* __restrict__ bitmap, uint32_t* __restrict__ row_epoch, uint32_t epoch)
+{
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t rs = run_start[j];
+        const uint32_t re = j + 1 < k ? run_start[j + 1] : (uint32_t)mb;
+        const uint32_t s = (uint32_t)(bkeys[rs] >> 32);
+        RunInfo ri;
+        ri.src = s; ri.rs = rs; ri.re = re; ri.off = off[s]; ri.end = off[s + 1];
+        runs[j] = ri;
+        atomicOr(bitmap + (s >> 5), 1u << (s & 31));
+        if (row_epoch) row_epoch[s] = epoch;   // the source's samplers are reset (wharfmh.h:504,539)
+    }
+}
+
+// new_off[v] = off[v] +/- (changing batch edges with src < v)
+__global__ void k_new_offsets(const uint64_t* __restrict__ off, uint64_t n, const uint64_t* __restrict__ bkeys,
+                              uint64_t mb, const uint32_t* __restrict__ cf, int insert, uint64_t* __restrict__ noff)
+{
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = v << 32;
+        uint64_t lo = 0, hi = mb;
+        while (lo < hi) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            if (bkeys[mid] < t) lo = mid + 1; else hi = mid;
+        }
+        const uint64_t c = cf[lo];
+        noff[v] = insert ? off[v] + c : off[v] - c;
+    }
+}
+
+// Move every old edge to its slot in the new CSR (one coalesced streaming pass).
+__global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint32_t* __restrict__ anc, uint64_t m,
+                             const RunInfo* __restrict__ runs, uint64_t k, const uint64_t* __restrict__ bkeys,
+                             const uint32_t* __restrict__ cf, const uint64_t* __restrict__ noff, int insert,
+                             uint32_t* __restrict__ nadj, uint32_t* __restrict__ nanc, uint64_t cap)
+{
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
+        // last source run whose row starts at or before e
+        uint64_t lo = 0, hi = k;
+        while (lo < hi) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            if (runs[mid].off <= e) lo = mid + 1; else hi = mid;
+        }
+        const uint32_t x = adj[e];
+        if (lo == 0) {
+            nadj[e] = x;
+            if (nanc) nanc[e] = anc[e];
+            continue;
+        }
+        const RunInfo ri = runs[lo - 1];
+        if (e < ri.end) {
+            // inside a source row: position = new row start + rank among survivors
+            uint64_t b = ri.rs, t = ri.re;
+            while (b < t) {
+                const uint64_t mid = b + ((t - b) >> 1);
+                if ((uint32_t)bkeys[mid] < x) b = mid + 1; else t = mid;
+            }
+            const uint64_t before = cf[b] - cf[ri.rs];
+            if (!insert && b < ri.re && (uint32_t)bkeys[b] == x) continue;   // deleted
+            const uint64_t np = noff[ri.src] + (e - ri.off) + (insert ? before : -(int64_t)before);
+            if (np >= cap) continue;   // never taken for a consistent CSR; keeps a bad input in bounds
+            nadj[np] = x;
+            if (nanc) nanc[np] = kAnchorNone;
+        } else {
+            const uint64_t shift = cf[ri.re];
+            const uint64_t np = insert ? e + shift : e - shift;
+            if (np >= cap) continue;
+            nadj[np] = x;
+            if (nanc) nanc[np] = anc[e];
+        }
+    }
+}
+
+// Place the inserted edges (insert only).
+__global__ void k_place_new(const uint64_t* __restrict__ bkeys, uint64_t mb, const uint32_t* __restrict__ chg,
+                            const uint32_t* __restrict__ cf, const uint32_t* __restrict__ run_start, uint64_t k,
+                            const RunInfo* __restrict__ runs, const uint32_t* __restrict__ adj,
+                            const uint64_t* __restrict__ noff, uint32_t* __restrict__ nadj, uint32_t* __restrict__ nanc,
+                            uint64_t cap)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mb; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (!chg[i]) continue;
+        uint64_t lo = 0, hi = k;
+        while (lo < hi) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            if (run_start[mid] <= i) lo = mid + 1; else hi = mid;
+        }
+        const RunInfo ri = runs[lo - 1];
+        const uint32_t d = (uint32_t)bkeys[i];
+        uint64_t b = ri.off, t = ri.end;
+        while (b < t) {
+            const uint64_t mid = b + ((t - b) >> 1);
+            if (adj[mid] < d) b = mid + 1; else t = mid;
+        }
+        const uint64_t np = noff[ri.src] + (cf[i] - cf[ri.rs]) + (b - ri.off);
+        if (np >= cap) continue;
+        nadj[np] = d;
+        if (nanc) nanc[np] = kAnchorNone;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// walk export / index
+// ---------------------------------------------------------------------------
+// [L][W] -> [W][L] through a 64x64 LDS tile (+1 pad against bank conflicts)
+__global__ void k_transpose(const uint32_t* __restrict__ in, uint64_t W, uint32_t L, uint32_t* __restrict__ out)
+{
+    __shared__ uint32_t tile[64][65];
+    const uint64_t w0 = (uint64_t)blockIdx.x * 64;
+    const uint32_t p0 = blockIdx.y * 64;
+    const uint32_t tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 256 threads: 4 rows per pass
+    for (uint32_t r = ty; r < 64; r += 4) {
+        const uint32_t p = p0 + r;
+        const uint64_t w = w0 + tx;
+        if (p < L && w < W) tile[r][tx] = in[(uint64_t)p * W + w];
+    }
+    __syncthreads();
+    for (uint32_t r = ty; r < 64; r += 4) {
+        const uint64_t w = w0 + r;
+        const uint32_t p = p0 + tx;
+        if (p < L && w < W) out[w * L + p] = tile[tx][r];
+    }
+}
+
+__global__ void k_gather_walk(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* __restrict__ out)
+{
+    for (uint32_t p = threadIdx.x; p < L; p += blockDim.x) out[p] = walks[(uint64_t)p * W + li];
+}
+
+// entries: sort key = (vertex << kb) | (wid*L + pos), value = next
+__global__ void k_index_entries(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc,
+                                uint64_t lo, int kb, const uint64_t* __restrict__ col_base,
+                                uint64_t* __restrict__ skeys, uint32_t* __restrict__ vals)
+{
+    for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = li / n_loc;
+        const uint64_t wid = r * n + lo + (li - r * n_loc);
+        uint64_t at = col_base[li];
+        for (uint32_t p = 0; p < L; p++) {
+            const uint32_t v = walks[(uint64_t)p * W + li];
+            if (v == kSent) break;
+            const uint32_t nx = p + 1 < L ? walks[(uint64_t)(p + 1) * W + li] : kSent;
+            skeys[at] = ((uint64_t)v << kb) | (wid * L + p);
+            vals[at] = nx;
+            at++;
+        }
+    }
+}
+
+__global__ void k_walk_lengths(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, uint64_t* __restrict__ len)
+{
+    for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t c = 0;
+        for (uint32_t p = 0; p < L; p++) {
+            if (walks[(uint64_t)p * W + li] == kSent) break;
+            c++;
+        }
+        len[li] = c;
+    }
+}
+
+__global__ void k_index_split(const uint64_t* __restrict__ skeys, uint64_t E, int kb, unsigned long long* __restrict__ counts,
+                              uint64_t* __restrict__ keys)
+{
+    const uint64_t mask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = skeys[i];
+        keys[i] = k & mask;
+        atomicAdd(counts + (k >> kb), 1ull);
+    }
+}
+
+__global__ void k_li_to_wid(const uint64_t* __restrict__ li, uint64_t cnt, uint64_t n, uint64_t n_loc, uint64_t lo,
+                            uint32_t* __restrict__ out)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t l = li[i];
+        const uint64_t r = l / n_loc;
+        out[i] = (uint32_t)(r * n + lo + (l - r * n_loc));
+    }
+}
+
+__global__ void k_fill_u32(uint32_t* __restrict__ p, uint64_t cnt, uint32_t v)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+
+// Szudzik pairing (walks/pairings.h:124-210); exact isqrt for 64-bit unpair
+__device__ __forceinline__ uint64_t isqrt64(uint64_t z)
+{
+    uint64_t s = (uint64_t)sqrt((double)z);
+    while (s * s > z) s--;
+    while ((s + 1) * (s + 1) <= z && (s + 1) < 0x100000000ull) s++;
+    return s;
+}
+
+__global__ void k_szudzik64(int op, uint64_t cnt, uint64_t* __restrict__ x, uint64_t* __restrict__ y, uint64_t* __restrict__ z)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (op == 0) {
+            const uint64_t a = x[i], b = y[i];
+            z[i] = b >= a ? b * (b + 1) + a : a * a + b;
+        } else {
+            const uint64_t v = z[i];
+            const uint64_t s = isqrt64(v);
+            const uint64_t t = v - s * s;
+            if (t < s) { x[i] = s; y[i] = t; } else { x[i] = t - s; y[i] = s; }
+        }
+    }
+}
+
+unsigned grid_for(uint64_t work, unsigned block)
+{
+    const uint64_t g = (work + block - 1) / block;
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(g, 256 * 64));
+}
+
+void launch_rmat_keys(const RmatParams& p, uint64_t M, int directed, uint64_t* keys, hipStream_t s)
+{ hipLaunchKernelGGL(k_rmat_keys, grid_for(M, 256), 256, 0, s, p, M, directed, keys); }
+void launch_pairs_to_keys(const uint32_t* pairs, uint64_t m, uint64_t n, uint64_t* keys, unsigned long long* err, hipStream_t s)
+{ hipLaunchKernelGGL(k_pairs_to_keys, grid_for(m, 256), 256, 0, s, pairs, m, n, keys, err); }
+void launch_csr_to_keys(const uint64_t* off, uint64_t n, const uint32_t* tgt, uint64_t* keys, unsigned long long* err, hipStream_t s)
+{ if (n) hipLaunchKernelGGL(k_csr_to_keys, (unsigned)((n + 63) / 64), 256, 0, s, off, n, tgt, keys, err); }
+void launch_unique_flags(const uint64_t* keys, uint64_t m, int drop_loops, uint8_t* keep, hipStream_t s)
+{ hipLaunchKernelGGL(k_unique_flags, grid_for(m, 256), 256, 0, s, keys, m, drop_loops, keep); }
+void launch_offsets_from_keys(const uint64_t* keys, uint64_t m, uint64_t n, uint64_t* off, hipStream_t s)
+{ hipLaunchKernelGGL(k_offsets_from_keys, grid_for(n + 1, 256), 256, 0, s, keys, m, n, off); }
+void launch_low32(const uint64_t* keys, uint64_t m, uint32_t* out, hipStream_t s)
+{ hipLaunchKernelGGL(k_low32, grid_for(m, 256), 256, 0, s, keys, m, out); }
+void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off, const uint32_t* adj, int insert, uint32_t* chg, hipStream_t s)
+{ hipLaunchKernelGGL(k_batch_change, grid_for(mb, 256), 256, 0, s, bkeys, mb, off, adj, insert, chg); }
+void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_t s)
+{ hipLaunchKernelGGL(k_run_flags, grid_for(mb, 256), 256, 0, s, bkeys, mb, f); }
+void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
+                     RunInfo* runs, uint32_t* bitmap, uint32_t* row_epoch, uint32_t epoch, hipStream_t s)
+{ hipLaunchKernelGGL(k_run_info, grid_for(k, 256), 256, 0, s, bkeys, run_start, k, mb, off, runs, bitmap, row_epoch, epoch); }
+void launch_new_offsets(const uint64_t* off, uint64_t n, const uint64_t* bkeys, uint64_t mb, const uint32_t* cf, int insert,
+                        uint64_t* noff, hipStream_t s)
+{ hipLaunchKernelGGL(k_new_offsets, grid_for(n + 1, 256), 256, 0, s, off, n, bkeys, mb, cf, insert, noff); }
+void launch_move_edges(const uint32_t* adj, const uint32_t* anc, uint64_t m, const RunInfo* runs, uint64_t k,
+                       const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
+                       uint32_t* nanc, uint64_t cap, hipStream_t s)
+{ if (m) hipLaunchKernelGGL(k_move_edges, grid_for(m, 256), 256, 0, s, adj, anc, m, runs, k, bkeys, cf, noff, insert, nadj, nanc, cap); }
+void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf, const uint32_t* run_start,
+                      uint64_t k, const RunInfo* runs, const uint32_t* adj, const uint64_t* noff, uint32_t* nadj,
+                      uint32_t* nanc, uint64_t cap, hipStream_t s)
+{ hipLaunchKernelGGL(k_place_new, grid_for(mb, 256), 256, 0, s, bkeys, mb, chg, cf, run_start, k, runs, adj, noff, nadj, nanc, cap); }
+void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s)
+{
+    if (!W) return;
+    const dim3 g((unsigned)((W + 63) / 64), (L + 63) / 64);
+    hipLaunchKernelGGL(k_transpose, g, 256, 0, s, in, W, L, out);
+}
+void launch_gather_walk(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* out, hipStream_t s)
+{ hipLaunchKernelGGL(k_gather_walk, 1, 256, 0, s, walks, W, L, li, out); }
+void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t* len, hipStream_t s)
+{ hipLaunchKernelGGL(k_walk_lengths, grid_for(W, 256), 256, 0, s, walks, W, L, len); }
+void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc, uint64_t lo, int kb,
+                          const uint64_t* col_base, uint64_t* skeys, uint32_t* vals, hipStream_t s)
+{ hipLaunchKernelGGL(k_index_entries, grid_for(W, 256), 256, 0, s, walks, W, L, n, n_loc, lo, kb, col_base, skeys, vals); }
+void launch_index_split(const uint64_t* skeys, uint64_t E, int kb, unsigned long long* counts, uint64_t* keys, hipStream_t s)
+{ hipLaunchKernelGGL(k_index_split, grid_for(E, 256), 256, 0, s, skeys, E, kb, counts, keys); }
+void launch_li_to_wid(const uint64_t* li, uint64_t cnt, uint64_t n, uint64_t n_loc, uint64_t lo, uint32_t* out, hipStream_t s)
+{ if (cnt) hipLaunchKernelGGL(k_li_to_wid, grid_for(cnt, 256), 256, 0, s, li, cnt, n, n_loc, lo, out); }
+void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s)
+{ if (cnt) hipLaunchKernelGGL(k_fill_u32, grid_for(cnt, 256), 256, 0, s, p, cnt, v); }
+void launch_szudzik64(int op, uint64_t cnt, uint64_t* x, uint64_t* y, uint64_t* z, hipStream_t s)
+{ if (cnt) hipLaunchKernelGGL(k_szudzik64, grid_for(cnt, 256), 256, 0, s, op, cnt, x, y, z); }
+
+}  // namespace wharf

@@ -1,0 +1,270 @@
+"""Python host mirror of dygrl::WharfMH (graph/wharfmh.h) over the HIP C ABI.
+
+Method names, argument order and meaning follow the reference class so driver
+code ports line by line:
+
+    reference (C++)                                     here
+    ------------------------------------------------    -----------------------------------------
+    WharfMH(n, m, offsets, edges)        wharfmh.h:58   WharfMH(n, m, offsets, edges, config=...)
+    WharfMH(n, m)                        wharfmh.h:26   WharfMH(n, 0)
+    number_of_vertices / number_of_edges :117 / :130    same
+    generate_initial_random_walks        :250           same
+    insert_edges_batch(m, edges, sorted, remove_dups,   insert_edges_batch(edges, sorted, remove_dups,
+        nn, apply_walk_updates, run_seq) :439               nn, apply_walk_updates, run_seq)
+    delete_edges_batch                   :588           same
+    walk(wid) -> "v0 v1 ... "            :365           same
+    vertex_at_walk(wid, pos)             :404           same
+    flatten_graph                        :175           flatten_graph() -> (offsets[n+1], targets[m])
+    destroy / destroy_index              :228 / :237    same
+    config::* globals                    globals.h      WharfConfig (per instance)
+
+Errors raise RuntimeError (the reference calls std::exit(1) / asserts).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+
+DEEPWALK, NODE2VEC = L.WHARF_DEEPWALK, L.WHARF_NODE2VEC
+RANDOM, BURNIN, WEIGHT = L.WHARF_INIT_RANDOM, L.WHARF_INIT_BURNIN, L.WHARF_INIT_WEIGHT
+SENTINEL = L.SENTINEL
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+@dataclass
+class WharfConfig:
+    """config::* (config/globals.h:7-29) plus the MH seed and the walk shard."""
+
+    walks_per_vertex: int = 10
+    walk_length: int = 80
+    model: int = DEEPWALK
+    paramP: float = 4.0
+    paramQ: float = 1.0
+    sampler_init: int = WEIGHT
+    deterministic: bool = True
+    seed: int = 0x5EED
+    shard_lo: int = 0
+    shard_hi: int = 0
+
+    def to_c(self) -> L.wharf_config:
+        c = L.wharf_config()
+        c.walks_per_vertex = self.walks_per_vertex
+        c.walk_length = self.walk_length
+        c.model = self.model
+        c.paramP = self.paramP
+        c.paramQ = self.paramQ
+        c.sampler_init = self.sampler_init
+        c.deterministic = int(bool(self.deterministic))
+        c.seed = self.seed & 0xFFFFFFFFFFFFFFFF
+        c.shard_lo = self.shard_lo
+        c.shard_hi = self.shard_hi
+        return c
+
+
+class WharfMH:
+    """Streaming random-walk engine: CSR snapshot + position-major walk matrix in HBM."""
+
+    def __init__(self, n: int, m: int = 0, offsets=None, edges=None, config: WharfConfig | None = None,
+                 device: int = 0, _handle=None):
+        self.config = config or WharfConfig()
+        self._cfg = self.config.to_c()
+        self.device = device
+        if _handle is not None:
+            self._h = _handle
+            return
+        h = C.c_void_p()
+        if m == 0 and offsets is None:
+            rc = L.lib.wharf_create_empty(C.byref(self._cfg), n, device, C.byref(h))
+        else:
+            off = np.ascontiguousarray(offsets, dtype=np.uint64)[:n]
+            tgt = np.ascontiguousarray(edges, dtype=np.uint32)
+            if len(off) != n or len(tgt) < m:
+                raise ValueError("offsets must have n entries and edges m entries")
+            rc = L.lib.wharf_create(C.byref(self._cfg), n, m, _ptr(off), _ptr(tgt), device, C.byref(h))
+        L.check(rc, None, "wharf_create")
+        self._h = h
+
+    @classmethod
+    def from_csr(cls, offsets_np1, targets, config: WharfConfig | None = None, device: int = 0) -> "WharfMH":
+        off = np.asarray(offsets_np1, dtype=np.uint64)
+        return cls(len(off) - 1, int(off[-1]), off[:-1], targets, config=config, device=device)
+
+    @classmethod
+    def from_rmat(cls, n: int, edges_number: int, vertices_number: int | None = None, seed: int = 0,
+                  a: float = 0.5, b: float = 0.2, c: float = 0.1, config: WharfConfig | None = None,
+                  device: int = 0) -> "WharfMH":
+        """Undirected RMAT base graph built on the device:
+        generate_batch_of_edges(edges_number, vertices_number, seed, false, false) (utility.h:55)."""
+        config = config or WharfConfig()
+        cfg = config.to_c()
+        h = C.c_void_p()
+        vn = vertices_number if vertices_number is not None else 2 * n
+        rc = L.lib.wharf_create_rmat(C.byref(cfg), n, edges_number, vn, seed, a, b, c, device, C.byref(h))
+        L.check(rc, None, "wharf_create_rmat")
+        return cls(n, config=config, device=device, _handle=h)
+
+    # -- lifetime ---------------------------------------------------------------------------
+    def destroy(self) -> None:
+        if getattr(self, "_h", None):
+            L.lib.wharf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+    def destroy_index(self) -> None:
+        L.check(L.lib.wharf_destroy_index(self._h), self._h, "destroy_index")
+
+    # -- queries ----------------------------------------------------------------------------
+    def number_of_vertices(self) -> int:
+        v = C.c_uint64()
+        L.check(L.lib.wharf_number_of_vertices(self._h, C.byref(v)), self._h, "number_of_vertices")
+        return v.value
+
+    def number_of_edges(self) -> int:
+        v = C.c_uint64()
+        L.check(L.lib.wharf_number_of_edges(self._h, C.byref(v)), self._h, "number_of_edges")
+        return v.value
+
+    def shard(self):
+        lo, hi, w = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        L.check(L.lib.wharf_shard(self._h, C.byref(lo), C.byref(hi), C.byref(w)), self._h, "shard")
+        return lo.value, hi.value, w.value
+
+    def set_shard(self, lo: int, hi: int) -> None:
+        """Own the walks of start vertices [lo, hi) (drops current walks)."""
+        L.check(L.lib.wharf_set_shard(self._h, lo, hi), self._h, "set_shard")
+        self.config.shard_lo, self.config.shard_hi = lo, hi
+
+    @property
+    def number_of_walks(self) -> int:
+        return self.shard()[2]
+
+    def stats(self) -> dict:
+        s = L.wharf_stats()
+        L.check(L.lib.wharf_get_stats(self._h, C.byref(s)), self._h, "stats")
+        return {k: getattr(s, k) for k, _ in L.wharf_stats._fields_}
+
+    def flatten_graph(self):
+        n, m = self.number_of_vertices(), self.number_of_edges()
+        off = np.zeros(n + 1, dtype=np.uint64)
+        adj = np.zeros(max(m, 1), dtype=np.uint32)
+        L.check(L.lib.wharf_get_graph(self._h, _ptr(off), _ptr(adj)), self._h, "flatten_graph")
+        return off, adj[:m]
+
+    # -- the walk path ------------------------------------------------------------------------
+    def generate_initial_random_walks(self) -> None:
+        L.check(L.lib.wharf_generate(self._h), self._h, "generate_initial_random_walks")
+
+    def _update(self, fn, edges, sorted, remove_dups, apply_walk_updates) -> np.ndarray:
+        e = np.ascontiguousarray(np.asarray(edges, dtype=np.uint32).reshape(-1, 2))
+        flags = (L.WHARF_SORTED if sorted else 0) | (L.WHARF_REMOVE_DUPS if remove_dups else 0) | \
+                (L.WHARF_APPLY_WALK_UPDATES if apply_walk_updates else 0)
+        out = np.zeros(max(self.number_of_walks, 1), dtype=np.uint32)
+        cnt = C.c_uint64()
+        L.check(fn(self._h, len(e), _ptr(e), flags, _ptr(out), C.byref(cnt)), self._h, fn.__name__)
+        return out[: cnt.value].copy()
+
+    def insert_edges_batch(self, edges, sorted: bool = False, remove_dups: bool = False, nn: int | None = None,
+                           apply_walk_updates: bool = True, run_seq: bool = False) -> np.ndarray:
+        """wharfmh.h:439.  `edges`: (m, 2) (src, dst).  Returns the affected walk ids
+        (ascending).  `nn` and `run_seq` are CPU-sort/scheduling hints of the
+        reference and have no effect here; the caller's buffer is not modified."""
+        return self._update(L.lib.wharf_insert_edges, edges, sorted, remove_dups, apply_walk_updates)
+
+    def delete_edges_batch(self, edges, sorted: bool = False, remove_dups: bool = False, nn: int | None = None,
+                           apply_walk_updates: bool = True, run_seq: bool = False) -> np.ndarray:
+        """wharfmh.h:588."""
+        return self._update(L.lib.wharf_delete_edges, edges, sorted, remove_dups, apply_walk_updates)
+
+    def walk(self, walk_id: int) -> str:
+        """WharfMH::walk (wharfmh.h:365): "v0 v1 ... " with a trailing space."""
+        n = C.c_size_t()
+        L.check(L.lib.wharf_walk_string(self._h, walk_id, None, 0, C.byref(n)), self._h, "walk")
+        buf = C.create_string_buffer(n.value + 1)
+        L.check(L.lib.wharf_walk_string(self._h, walk_id, buf, n.value + 1, C.byref(n)), self._h, "walk")
+        return buf.value.decode()
+
+    def walk_vertices(self, walk_id: int) -> np.ndarray:
+        out = np.zeros(self.config.walk_length, dtype=np.uint32)
+        ln = C.c_uint32()
+        L.check(L.lib.wharf_walk(self._h, walk_id, _ptr(out), C.byref(ln)), self._h, "walk")
+        return out[: ln.value]
+
+    def vertex_at_walk(self, walk_id: int, position: int) -> int:
+        v = C.c_uint32()
+        L.check(L.lib.wharf_vertex_at_walk(self._h, walk_id, position, C.byref(v)), self._h, "vertex_at_walk")
+        return v.value
+
+    def walks(self, layout: str = "walk") -> np.ndarray:
+        """The owned corpus, SENTINEL-padded: 'walk' -> [walks][L], 'position' -> [L][walks]."""
+        W, Lw = self.number_of_walks, self.config.walk_length
+        if layout == "walk":
+            out = np.zeros((W, Lw), dtype=np.uint32)
+            L.check(L.lib.wharf_export_walks(self._h, _ptr(out), 0), self._h, "export_walks")
+        else:
+            out = np.zeros((Lw, W), dtype=np.uint32)
+            L.check(L.lib.wharf_export_walks(self._h, _ptr(out), 1), self._h, "export_walks")
+        return out
+
+    def walk_ids(self) -> np.ndarray:
+        out = np.zeros(max(self.number_of_walks, 1), dtype=np.uint32)
+        L.check(L.lib.wharf_walk_ids(self._h, _ptr(out)), self._h, "walk_ids")
+        return out[: self.number_of_walks]
+
+    def export_walks_device(self, device_ptr: int, layout: str = "walk") -> None:
+        L.check(L.lib.wharf_export_walks_device(self._h, C.c_void_p(device_ptr), 0 if layout == "walk" else 1),
+                self._h, "export_walks_device")
+
+    def inverted_index(self):
+        """Per-vertex ascending (key = wid*L + pos, next) lists (walks/inverted_index.h):
+        returns (counts[n], keys, nexts)."""
+        sz = C.c_uint64()
+        L.check(L.lib.wharf_index_size(self._h, C.byref(sz)), self._h, "index_size")
+        n = self.number_of_vertices()
+        counts = np.zeros(n, dtype=np.uint64)
+        keys = np.zeros(max(sz.value, 1), dtype=np.uint64)
+        nexts = np.zeros(max(sz.value, 1), dtype=np.uint32)
+        L.check(L.lib.wharf_export_index(self._h, _ptr(counts), _ptr(keys), _ptr(nexts)), self._h, "export_index")
+        return counts, keys[: sz.value], nexts[: sz.value]
+
+
+def generate_batch_of_edges(edges_number: int, vertices_number: int, batch_seed: int, self_loops: bool = False,
+                            directed: bool = True, a: float = 0.5, b: float = 0.2, c: float = 0.1,
+                            device: int = 0) -> np.ndarray:
+    """utility::generate_batch_of_edges (utils/utility.h:55-146) on the device -> (k, 2) uint32."""
+    cap = edges_number * (1 if directed else 2)
+    out = np.zeros((max(cap, 1), 2), dtype=np.uint32)
+    cnt = C.c_uint64()
+    L.check(L.lib.wharf_generate_batch_of_edges(device, edges_number, vertices_number, batch_seed, int(self_loops),
+                                                int(directed), a, b, c, _ptr(out), C.byref(cnt)),
+            None, "generate_batch_of_edges")
+    return out[: cnt.value].copy()
+
+
+def szudzik64_pair(x, y, device: int = 0) -> np.ndarray:
+    """pairings::Szudzik<uint64_t>::pair (walks/pairings.h:124-176), elementwise on the device."""
+    x = np.ascontiguousarray(x, dtype=np.uint64).copy()
+    y = np.ascontiguousarray(y, dtype=np.uint64).copy()
+    z = np.zeros_like(x)
+    L.check(L.lib.wharf_szudzik64(device, 0, len(x), _ptr(x), _ptr(y), _ptr(z)), None, "szudzik64")
+    return z
+
+
+def szudzik64_unpair(z, device: int = 0):
+    """pairings::Szudzik<uint64_t>::unpair (walks/pairings.h:197-210) with an exact integer sqrt."""
+    z = np.ascontiguousarray(z, dtype=np.uint64).copy()
+    x = np.zeros_like(z)
+    y = np.zeros_like(z)
+    L.check(L.lib.wharf_szudzik64(device, 1, len(z), _ptr(x), _ptr(y), _ptr(z)), None, "szudzik64")
+    return x, y

@@ -1,0 +1,180 @@
+/*
+ * wharf_gpu.h — C ABI of the MI355X-native WharfMH walk engine.
+ *
+ * This is the drop-in boundary for the reference's walk-generation and
+ * incremental re-walk path (djordjijeK/DynamicGraphRepresentationLearning,
+ * graph/wharfmh.h).  Every entry point names the reference interface it
+ * replaces.  Plain pointers and sizes only; no C++ or torch types.
+ *
+ * Conventions
+ *   - every call returns 0 (WHARF_OK) or a negative WHARF_E* code; the message
+ *     is available from wharf_last_error(handle) (handle may be NULL for errors
+ *     raised before a handle exists).  The reference exits or asserts instead
+ *     (wharfmh.h:270,758; utility.h:220 divides by zero).
+ *   - input buffers are host memory owned by the caller and copied on entry
+ *     (the reference takes ownership of the CSR, wharfmh.h:99-103, and sorts the
+ *     caller's edge batch in place, wharfmh.h:450-453; this ABI does neither).
+ *   - output buffers are caller-allocated host memory; sizes are queried first.
+ *   - one host thread per handle; a handle owns one HIP device and one stream.
+ *     Calls are synchronous (they return after the device work completed).
+ *   - the graph, the walk matrix and all scratch stay resident in HBM between
+ *     calls.
+ */
+#ifndef WHARF_GPU_H
+#define WHARF_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WHARF_ABI_VERSION 1
+
+enum {
+    WHARF_OK = 0,
+    WHARF_E_INVALID = -1,   /* bad argument (sizes, ids >= n, null pointers) */
+    WHARF_E_HIP = -2,       /* HIP runtime error */
+    WHARF_E_NOMEM = -3,     /* device allocation failed */
+    WHARF_E_STATE = -4,     /* call not valid in the current state */
+    WHARF_E_RANGE = -5      /* walk id / position out of range or not owned by this shard */
+};
+
+/* types::RandomWalkModelType (config/types.h:28) */
+enum { WHARF_DEEPWALK = 0, WHARF_NODE2VEC = 1 };
+/* types::SamplerInitStartegy (config/types.h:31) */
+enum { WHARF_INIT_RANDOM = 0, WHARF_INIT_BURNIN = 1, WHARF_INIT_WEIGHT = 2 };
+/* insert_edges_batch / delete_edges_batch boolean arguments (wharfmh.h:439,588) */
+enum { WHARF_SORTED = 1, WHARF_REMOVE_DUPS = 2, WHARF_APPLY_WALK_UPDATES = 4 };
+
+#define WHARF_SENTINEL 0xFFFFFFFEu  /* std::numeric_limits<uint32_t>::max() - 1 (wharfmh.h:282) */
+
+/* The reference's mutable globals (config/globals.h:7-29) as a POD. */
+typedef struct wharf_config {
+    uint32_t walks_per_vertex;  /* config::walks_per_vertex (u8 in the reference), default 10 */
+    uint32_t walk_length;       /* config::walk_length (u8), default 80, 2..255 */
+    int32_t  model;             /* config::random_walk_model, default WHARF_DEEPWALK */
+    float    paramP;            /* config::paramP, default 4.0 */
+    float    paramQ;            /* config::paramQ, default 1.0 */
+    int32_t  sampler_init;      /* config::sampler_init_strategy, default WHARF_INIT_WEIGHT */
+    int32_t  deterministic;     /* config::deterministic_mode, default 1 */
+    uint64_t seed;              /* MH-mode Philox key (replaces config::random(time(nullptr))), default 0x5EED */
+    uint64_t shard_lo;          /* walks of start vertices [shard_lo, shard_hi) live on this handle; */
+    uint64_t shard_hi;          /*   shard_hi == 0 means all vertices */
+} wharf_config;
+
+typedef struct wharf_stats {
+    uint64_t n, m;                 /* number_of_vertices(), number_of_edges() (wharfmh.h:117,130) */
+    uint64_t walks;                /* walks owned by this handle */
+    uint64_t steps;                /* transitions appended by the last generate/update */
+    uint64_t accepts;              /* MH acceptances in the last generate/update */
+    uint64_t affected;             /* walks re-walked by the last update */
+    uint64_t batch_edges;          /* edges in the last batch after sort/dedup */
+    double   last_walk_kernel_ms;  /* device time of the last walk / re-walk kernel (HIP events) */
+    double   last_graph_update_ms; /* device time of the last CSR update (graph_update_time_on_*, config.h:10-14) */
+    double   last_walk_update_ms;  /* device time of the last scan + re-walk (walk_update_time_on_*) */
+    double   last_total_ms;        /* host wall time of the last call */
+    uint64_t hbm_bytes_walks;      /* resident bytes: walk matrix */
+    uint64_t hbm_bytes_graph;      /* resident bytes: CSR + vertex records (+ anchors) */
+} wharf_stats;
+
+typedef struct wharf_handle wharf_handle;
+
+void        wharf_config_default(wharf_config* cfg);
+const char* wharf_last_error(const wharf_handle* h);
+int         wharf_abi_version(void);
+int         wharf_device_count(int* count);
+
+/* WharfMH(long n, long m, uintE* offsets, uintV* edges, bool free_memory) (wharfmh.h:58-110).
+ * offsets: n entries (row v = [offsets[v], offsets[v+1]) with offsets[n] := m), targets: m.
+ * Rows are canonicalised (sorted ascending, duplicates removed), the form
+ * CompressedEdges::get_edges returns (tree_plus.h:233-243). */
+int wharf_create(const wharf_config* cfg, uint64_t n, uint64_t m, const uint64_t* offsets,
+                 const uint32_t* targets, int device, wharf_handle** out);
+
+/* WharfMH(long n, long m) (wharfmh.h:26-47): n isolated vertices. */
+int wharf_create_empty(const wharf_config* cfg, uint64_t n, int device, wharf_handle** out);
+
+/* A synthetic base graph built on the device without a host round trip:
+ * the undirected RMAT graph utility::generate_batch_of_edges(edges_number,
+ * vertices_number, seed, self_loops=false, directed=false, a, b, c)
+ * (utils/utility.h:55-146) on n vertices (n >= the RMAT size). */
+int wharf_create_rmat(const wharf_config* cfg, uint64_t n, uint64_t edges_number, uint64_t vertices_number,
+                      uint64_t seed, double a, double b, double c, int device, wharf_handle** out);
+
+/* ~WharfMH / WharfMH::destroy (wharfmh.h:228). */
+int wharf_destroy(wharf_handle* h);
+/* WharfMH::destroy_index (wharfmh.h:237): drops every walk. */
+int wharf_destroy_index(wharf_handle* h);
+
+/* WharfMH::generate_initial_random_walks (wharfmh.h:250-356). */
+int wharf_generate(wharf_handle* h);
+
+/* WharfMH::insert_edges_batch / delete_edges_batch (wharfmh.h:439-726) followed,
+ * when WHARF_APPLY_WALK_UPDATES is set, by batch_walk_update (733-923).
+ * pairs: m (src, dst) u32 pairs.  affected_out (may be NULL) receives the
+ * affected walk ids in ascending order (the reference returns them in hash
+ * order); capacity >= the owned walk count.  *n_affected receives the count. */
+int wharf_insert_edges(wharf_handle* h, uint64_t m, const uint32_t* pairs, uint32_t flags,
+                       uint32_t* affected_out, uint64_t* n_affected);
+int wharf_delete_edges(wharf_handle* h, uint64_t m, const uint32_t* pairs, uint32_t flags,
+                       uint32_t* affected_out, uint64_t* n_affected);
+
+/* number_of_vertices / number_of_edges (wharfmh.h:117-133). */
+int wharf_number_of_vertices(const wharf_handle* h, uint64_t* n);
+int wharf_number_of_edges(const wharf_handle* h, uint64_t* m);
+/* walks owned by this handle and the [lo, hi) start-vertex shard. */
+int wharf_shard(const wharf_handle* h, uint64_t* lo, uint64_t* hi, uint64_t* walks);
+
+/* Re-partition the walks: this handle owns the walks of start vertices
+ * [lo, hi) (hi == 0: all).  Drops the current walks (like destroy_index). */
+int wharf_set_shard(wharf_handle* h, uint64_t lo, uint64_t hi);
+
+/* flatten_graph (wharfmh.h:175-208): offsets_out n+1 entries, targets_out m. */
+int wharf_get_graph(wharf_handle* h, uint64_t* offsets_out, uint32_t* targets_out);
+
+/* WharfMH::walk / vertex_at_walk (wharfmh.h:365-427).
+ * wharf_walk: vertices of walk `wid` into out (capacity walk_length), *len = count. */
+int wharf_walk(wharf_handle* h, uint64_t wid, uint32_t* out, uint32_t* len);
+/* text form "v0 v1 ... " (trailing space), *len excludes the terminating NUL. */
+int wharf_walk_string(wharf_handle* h, uint64_t wid, char* buf, size_t cap, size_t* len);
+int wharf_vertex_at_walk(wharf_handle* h, uint64_t wid, uint32_t position, uint32_t* vertex);
+
+/* Whole corpus of this handle's walks, SENT-padded.
+ *   layout 0: walk-major [walks][walk_length], rows in ascending walk id
+ *   layout 1: position-major [walk_length][walks] (the resident HBM layout)
+ * dst: host buffer of walks*walk_length u32; or, with wharf_export_walks_device,
+ * a device pointer on the handle's device (used for the RCCL corpus gather). */
+int wharf_export_walks(wharf_handle* h, uint32_t* dst, int layout);
+int wharf_export_walks_device(wharf_handle* h, uint32_t* dst_device, int layout);
+/* global walk id of each owned walk, in export row order (walks entries). */
+int wharf_walk_ids(wharf_handle* h, uint32_t* ids_out);
+
+/* The inverted index (walks/inverted_index.h:12-93): for each vertex v the
+ * ascending (key = wid*walk_length + pos, next) entries of the walks owned by
+ * this handle; next = SENT at the last position.
+ * First call wharf_index_size, then wharf_export_index with counts[n],
+ * keys[size], nexts[size]. */
+int wharf_index_size(wharf_handle* h, uint64_t* size);
+int wharf_export_index(wharf_handle* h, uint64_t* counts, uint64_t* keys, uint32_t* nexts);
+
+int wharf_get_stats(const wharf_handle* h, wharf_stats* out);
+
+/* utility::generate_batch_of_edges (utils/utility.h:55-146) on the device:
+ * sorted, deduplicated (src,dst) pairs.  out_pairs capacity: 2*edges_number
+ * pairs when undirected, edges_number otherwise. */
+int wharf_generate_batch_of_edges(int device, uint64_t edges_number, uint64_t vertices_number, uint64_t batch_seed,
+                                  int self_loops, int directed, double a, double b, double c,
+                                  uint32_t* out_pairs, uint64_t* count);
+
+/* pairings::Szudzik (walks/pairings.h:113-226) on the device, elementwise.
+ * op 0: pair(x[i], y[i]) -> z[i]; op 1: unpair(z[i]) -> x[i], y[i].  64-bit
+ * unpair uses an exact integer square root (the reference's floor(sqrt(double))
+ * is only exact below 2^52). */
+int wharf_szudzik64(int device, int op, uint64_t count, uint64_t* x, uint64_t* y, uint64_t* z);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WHARF_GPU_H */

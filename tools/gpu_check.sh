@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, a short bench.  Every GPU step has
+# its own time limit; a crash/abort/timeout ends the session (no retries).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider -rf ;;
+    smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench18) step bench_s18 600 python bench.py --scale 18 --samples 7324270 --steps 3 --warmup 1 --cpu-baseline off ;;
+    bench)  step bench 900 python bench.py ;;
+  esac
+done
