@@ -417,6 +417,11 @@ uint64_t wo_update(wo_engine* e, int insert, uint64_t m, const uint32_t* pairs_i
         k++;
     }
     m = k;
+    e->accepts = e->steps = 0;
+    if (m == 0) {   /* nothing to apply: no sources, no sampler reset, epoch unchanged */
+        free(b);
+        return 0;
+    }
 
     /* batch sources: every distinct source, whether or not its row changes */
     uint8_t* is_src = (uint8_t*)calloc(e->n ? e->n : 1, 1);
