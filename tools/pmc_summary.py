@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 outputs for one kernel into profiles/.
+
+    python tools/pmc_summary.py --tag gen_deepwalk_mh_s22 --kernel "k_walk<wharf::VRec32, 0, false, false>" \
+        --fetch gpurun_out/pmc_fetch/run_counter_collection.csv \
+        --write gpurun_out/pmc_write/run_counter_collection.csv \
+        --stats gpurun_out/prof_gen/run_kernel_stats.csv --round r01
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB, collected in separate passes; on gfx950 FETCH_SIZE
+counts 64 B per TCC_EA0_RDREQ while the requests are 128 B, so the read side
+is doubled (the guide's correction for wide reads; our gathers miss whole
+lines, so the same factor is applied and the raw value is kept beside it).
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_launch(path, kernel, counter):
+    vals = []
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--kernel", required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--stats", required=True)
+    ap.add_argument("--round", default="r01")
+    ap.add_argument("--algorithmic-bytes", type=float, default=None)
+    a = ap.parse_args()
+    f = per_launch(a.fetch, a.kernel, "FETCH_SIZE")
+    w = per_launch(a.write, a.kernel, "WRITE_SIZE")
+    avg_ns = None
+    for r in csv.DictReader(open(a.stats)):
+        if a.kernel in r["Name"]:
+            avg_ns = float(r["AverageNs"])
+            break
+    fetch_raw = statistics.mean(f) * 1024
+    write = statistics.mean(w) * 1024
+    out = {
+        "kernel": a.kernel,
+        "launches": {"fetch_pass": len(f), "write_pass": len(w)},
+        "fetch_size_bytes_raw": fetch_raw,
+        "fetch_bytes_corrected": 2 * fetch_raw,
+        "write_bytes": write,
+        "hbm_bytes_per_launch": 2 * fetch_raw + write,
+        "avg_kernel_ns_kernel_trace": avg_ns,
+        "effective_GBps": (2 * fetch_raw + write) / avg_ns if avg_ns else None,
+        "algorithmic_bytes_per_launch": a.algorithmic_bytes,
+        "sources": [os.path.relpath(p, REPO) for p in (a.fetch, a.write, a.stats)],
+    }
+    dst = os.path.join(REPO, "profiles", f"pmc_{a.tag}.json")
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
