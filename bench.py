@@ -50,7 +50,8 @@ def parse():
     p.add_argument("--paramP", type=float, default=0.5)
     p.add_argument("--paramQ", type=float, default=2.0)
     p.add_argument("--det", action="store_true", help="deterministic mode instead of MH")
-    p.add_argument("--rewalk-batches", type=int, default=3, help="10k-edge insert batches timed after the bench")
+    p.add_argument("--rewalk-batches", type=int, default=50, help="10k-edge insert batches (configs[2])")
+    p.add_argument("--stream-samples", type=int, default=43_000_000, help="configs[2] base graph undirected samples")
     p.add_argument("--cpu-baseline", choices=["auto", "reference", "port", "off"], default="auto")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-timeout", type=int, default=300)
@@ -187,24 +188,46 @@ def main():
     tag = f"gen_{args.model}_{'det' if args.det else 'mh'}_s{args.scale}"
 
     # re-walk latency: 10k-edge batches (generate_batch_of_edges(5000, n, b, false, undirected))
+    g.destroy()
+
+    # configs[2]: soc-LiveJournal-sized streaming, 10k-edge insert batches
+    # (memory-throughput-latency.cpp:126-134: generate_batch_of_edges(5000, n, seed=b, false, undirected))
     rewalk = None
     if args.rewalk_batches > 0:
-        lat, aff, gu, wu = [], [], [], []
+        gs = W.WharfMH.from_rmat(n, args.stream_samples, 2 * n, seed=args.seed + 1, config=cfg, device=local)
+        gs.set_shard(lo, hi) if world == 1 else gs.set_shard(*balanced_shards(
+            np.diff(gs.flatten_graph()[0].astype(np.int64)), world)[rank])
+        gs.generate_initial_random_walks()
+        out = np.empty(gs.number_of_walks, dtype=np.uint32)
+        lat, aff, gu, wu, kern = [], [], [], [], []
         for b in range(args.rewalk_batches):
             batch = W.generate_batch_of_edges(5000, n, b, False, False, device=local)
             barrier()
             t1 = time.perf_counter()
-            a = g.insert_edges_batch(batch, remove_dups=True)
+            a = gs.insert_edges_batch(batch, remove_dups=True, out=out)
             barrier()
             lat.append((time.perf_counter() - t1) * 1e3)
-            s2 = g.stats()
+            s2 = gs.stats()
             aff.append(len(a))
             gu.append(s2["last_graph_update_ms"])
             wu.append(s2["last_walk_update_ms"])
-        rewalk = {"batches": args.rewalk_batches, "edges_per_batch": int(len(batch)),
-                  "latency_ms": [round(x, 3) for x in lat], "median_ms": round(float(np.median(lat)), 3),
-                  "affected_walks_rank": aff, "graph_update_ms": [round(x, 3) for x in gu],
-                  "walk_update_ms": [round(x, 3) for x in wu]}
+            kern.append(s2["last_walk_kernel_ms"])
+        lat_all = lat
+        if dist:
+            tl = torch.tensor(lat, dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(tl, op=dist.ReduceOp.MAX)
+            lat_all = tl.tolist()
+        rewalk = {"workload": f"configs[2] soc-LiveJournal-sized streaming: RMAT scale {args.scale}, "
+                              f"{args.stream_samples} undirected samples (m={gs.number_of_edges()}), "
+                              f"{args.rewalk_batches} insert batches of generate_batch_of_edges(5000, n, b, false, "
+                              f"undirected), re-walk applied",
+                  "batches": args.rewalk_batches, "edges_per_batch": int(len(batch)),
+                  "median_ms": round(float(np.median(lat_all)), 3), "p90_ms": round(float(np.percentile(lat_all, 90)), 3),
+                  "mean_affected_walks_rank0": int(np.mean(aff)),
+                  "median_graph_update_ms": round(float(np.median(gu)), 3),
+                  "median_walk_update_ms": round(float(np.median(wu)), 3),
+                  "median_rewalk_kernel_ms": round(float(np.median(kern)), 3)}
+        gs.destroy()
 
     if rank == 0:
         achieved = (steps_local * bytes_per_step / (avg_kernel_ms * 1e-3) / 1e9) if bytes_per_step else None
@@ -237,12 +260,9 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and args.cpu_baseline != "off":
-            if off is None:
-                off, adj = g.flatten_graph()
             active = int((deg > 0).sum())
             line["cpu_baseline"] = cpu_baseline(args, n, active, off, adj, args.cpu_baseline)
         print(json.dumps(line), flush=True)
-    g.destroy()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -82,9 +82,9 @@ struct wharf_handle {
     wharf_config cfg{};
     uint64_t n = 0, m = 0, lo = 0, hi = 0, n_loc = 0, W = 0;
     uint32_t L = 0, wpv = 0;
-    bool wide = false, anchors = false, has_walks = false;
+    bool anchors = false, has_walks = false;
     uint32_t epoch = 0;
-    DevBuf off, adj, vrec, anchor, row_epoch, off2, adj2, anchor2;
+    DevBuf off, adj, vrec, erec, anchor, row_epoch, off2, adj2, anchor2;
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
     DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, count, pairs, sel;
     wharf_stats st{};
@@ -137,9 +137,7 @@ struct wharf_handle {
 
     void finish_graph()
     {
-        wide = m >= (1ull << 32);
-        vrec.ensure(std::max<uint64_t>(n, 1) * (wide ? sizeof(VRec64) : sizeof(VRec32)));
-        launch_vrec(off.as<uint64_t>(), n, vrec.p, wide, s);
+        build_records();
         row_epoch.ensure(std::max<uint64_t>(n, 1) * 4);
         HIPCHK(hipMemsetAsync(row_epoch.p, 0, std::max<uint64_t>(n, 1) * 4, s));
         if (anchors) {
@@ -160,11 +158,21 @@ struct wharf_handle {
         has_walks = false;
     }
 
+    // vertex rows and per-slot edge records (one 16-B gather per walk step)
+    void build_records()
+    {
+        vrec.ensure(std::max<uint64_t>(n, 1) * sizeof(ERec));
+        erec.ensure(std::max<uint64_t>(m, 1) * sizeof(ERec));
+        launch_vrec(off.as<uint64_t>(), n, vrec.as<ERec>(), s);
+        launch_erec(adj.as<uint32_t>(), m, vrec.as<ERec>(), erec.as<ERec>(), s);
+    }
+
     WalkArgs walk_args()
     {
         ensure_walks();
         WalkArgs a{};
-        a.vrec = vrec.p;
+        a.vrec = vrec.as<ERec>();
+        a.erec = erec.as<ERec>();
         a.adj = adj.as<uint32_t>();
         a.anchor = anchors ? anchor.as<uint32_t>() : nullptr;
         a.row_epoch = row_epoch.as<uint32_t>();
@@ -279,7 +287,7 @@ void free_handle(wharf_handle* h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->s) (void)hipStreamSynchronize(h->s);
-    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->anchor, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
+    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->anchor, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
                       &h->aff, &h->rtab, &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags,
                       &h->chg, &h->cf, &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel})
         b->release();
@@ -399,13 +407,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         std::swap(h->adj, h->adj2);
         if (h->anchors) std::swap(h->anchor, h->anchor2);
         h->m = m_new;
-        const bool wide_new = m_new >= (1ull << 32);
-        if (wide_new != h->wide) {
-            h->wide = wide_new;
-            h->vrec.release();
-            h->vrec.ensure(h->n * (h->wide ? sizeof(VRec64) : sizeof(VRec32)));
-        }
-        launch_vrec(h->off.as<uint64_t>(), h->n, h->vrec.p, h->wide, s);
+        h->build_records();
         HIPCHK(hipEventRecord(h->ev[1], s));
 
         // 5. rewalk points + suffix re-walk in one pass over the walk matrix
@@ -415,7 +417,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             WalkArgs a = h->walk_args();
             HIPCHK(hipEventRecord(h->ev[2], s));
             a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
-            launch_walk(a, h->wide, true, s);
+            launch_walk(a, true, s);
             HIPCHK(hipEventRecord(h->ev[3], s));
             // ascending affected walk ids
             h->sel.ensure(h->W * 8);
@@ -567,7 +569,7 @@ int wharf_generate(wharf_handle* h)
         HIPCHK(hipMemsetAsync(h->counters.p, 0, 16, h->s));
         WalkArgs a = h->walk_args();
         HIPCHK(hipEventRecord(h->ev[0], h->s));
-        launch_walk(a, h->wide, false, h->s);
+        launch_walk(a, false, h->s);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(h->ev[1], h->s));
         h->read_counters();
@@ -823,7 +825,7 @@ int wharf_get_stats(const wharf_handle* h, wharf_stats* out)
     out->m = h->m;
     out->walks = h->W;
     out->hbm_bytes_walks = h->W * h->L * 4;
-    out->hbm_bytes_graph = (h->n + 1) * 8 + h->m * 4 + h->n * (h->wide ? 16 : 8) + (h->anchors ? h->m * 4 : 0);
+    out->hbm_bytes_graph = (h->n + 1) * 8 + h->m * 4 + (h->n + h->m) * sizeof(ERec) + (h->anchors ? h->m * 4 : 0);
     return WHARF_OK;
 }
 

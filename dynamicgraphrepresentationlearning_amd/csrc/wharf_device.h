@@ -21,11 +21,13 @@ constexpr uint32_t kNoRewalk = 0xFFu;          // rewalk position "none"
 // Philox counter word 3 = (epoch << 4) | stream
 enum : uint32_t { kStreamStep = 0, kStreamAnchor = 1, kStreamBurnin = 2, kStreamPrev = 3 };
 
-// CSR vertex record: one aligned load gives a row's start and length.
-struct VRec32 { uint32_t off, deg; };                 // m < 2^32
-struct alignas(16) VRec64 { uint64_t off, deg; };     // m >= 2^32
-
-template <class VR> __device__ __forceinline__ VR load_vrec(const VR* p, uint32_t v) { return p[v]; }
+// Row record: a vertex and its CSR row.  vrec[v] = {v, deg(v), off(v)};
+// erec[e] = vrec[adj[e]], so a walk step reads its next vertex AND that
+// vertex's row with one aligned 16-B load.
+struct alignas(16) ERec {
+    uint32_t v, deg;
+    uint64_t off;
+};
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (Random123); 10 rounds, key bumped between rounds.

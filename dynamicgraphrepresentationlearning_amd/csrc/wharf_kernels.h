@@ -15,8 +15,9 @@ enum { kDeepWalk = 0, kNode2Vec = 1 };
 enum { kInitRandom = 0, kInitBurnin = 1, kInitWeight = 2 };
 
 struct WalkArgs {
-    const void* vrec;            // VRec32[n] or VRec64[n]
-    const uint32_t* adj;         // CSR targets
+    const ERec* vrec;            // [n]: the row of each vertex
+    const ERec* erec;            // [m]: per CSR slot, the target's row
+    const uint32_t* adj;         // [m]: CSR targets (binary searches, anchor proposals)
     uint32_t* anchor;            // MH anchors per CSR slot (node2vec MH), else null
     const uint32_t* row_epoch;   // epoch of each row's last sampler reset (MH)
     uint32_t* walks;             // [L][W]
@@ -39,8 +40,9 @@ struct RunInfo {
 
 unsigned grid_for(uint64_t work, unsigned block);
 
-void launch_walk(const WalkArgs& a, bool wide, bool rewalk, hipStream_t s);
-void launch_vrec(const uint64_t* off, uint64_t n, void* vrec, bool wide, hipStream_t s);
+void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s);
+void launch_vrec(const uint64_t* off, uint64_t n, ERec* vrec, hipStream_t s);
+void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, hipStream_t s);
 void launch_rmat_keys(const RmatParams& p, uint64_t M, int directed, uint64_t* keys, hipStream_t s);
 void launch_pairs_to_keys(const uint32_t* pairs, uint64_t m, uint64_t n, uint64_t* keys, unsigned long long* err, hipStream_t s);
 void launch_csr_to_keys(const uint64_t* off, uint64_t n, const uint32_t* tgt, uint64_t* keys, unsigned long long* err, hipStream_t s);

@@ -21,20 +21,8 @@ __device__ __forceinline__ void wave_add(unsigned long long* dst, uint32_t v)
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, (unsigned long long)v);
 }
 
-template <class VR>
-__device__ __forceinline__ bool row_contains(const uint32_t* __restrict__ adj, const VR& r, uint32_t x)
-{
-    // std::binary_search over the ascending row (node2vec.h:112-119)
-    uint64_t lo = r.off, hi = r.off + r.deg;
-    while (lo < hi) {
-        const uint64_t mid = lo + ((hi - lo) >> 1);
-        if (adj[mid] < x) lo = mid + 1; else hi = mid;
-    }
-    return lo < r.off + r.deg && adj[lo] == x;
-}
-
-template <class VR>
-__device__ __forceinline__ int64_t row_find(const uint32_t* __restrict__ adj, const VR& r, uint32_t x)
+// std::binary_search over the ascending row (node2vec.h:112-119)
+__device__ __forceinline__ int64_t row_find(const uint32_t* __restrict__ adj, const ERec& r, uint32_t x)
 {
     uint64_t lo = r.off, hi = r.off + r.deg;
     while (lo < hi) {
@@ -44,45 +32,38 @@ __device__ __forceinline__ int64_t row_find(const uint32_t* __restrict__ adj, co
     return (lo < r.off + r.deg && adj[lo] == x) ? (int64_t)lo : -1;
 }
 
-template <class VR>
-__device__ __forceinline__ uint64_t pick(uint32_t r, const VR& rec)
-{
-    if constexpr (sizeof(VR) == 8) return pick32(r, (uint32_t)rec.deg);
-    else return pick64(r, rec.deg);
-}
-
-// node2vec.h:74-88 (DeepWalk: deepwalk.h:67-70 returns 1)
-template <int MODEL, class VR>
-__device__ __forceinline__ float weight(const WalkArgs& a, uint32_t prev, const VR& rprev, uint32_t c)
+// node2vec.h:74-88 (DeepWalk: deepwalk.h:67-70 returns 1); rprev = row of prev
+template <int MODEL>
+__device__ __forceinline__ float weight(const WalkArgs& a, const ERec& rprev, uint32_t c)
 {
     if constexpr (MODEL == kDeepWalk) return 1.0f;
-    if (c == prev) return a.inv_p;
-    if (row_contains(a.adj, rprev, c)) return 1.0f;
+    if (c == rprev.v) return a.inv_p;
+    if (row_find(a.adj, rprev, c) >= 0) return 1.0f;
     return a.inv_q;
 }
 
 // MetropolisHastingsSampler::init (metropolis_hastings_sampler.h:69-108) with
-// proposals from the (cur, prev, row_epoch[cur]) Philox stream.
-template <class VR>
-__device__ uint32_t anchor_init(const WalkArgs& a, uint32_t cur, const VR& rcur, uint32_t prev, const VR& rprev)
+// proposals from the (cur, prev, row_epoch[cur]) Philox stream.  Returns the
+// anchor as a slot of cur's row.
+__device__ uint32_t anchor_init(const WalkArgs& a, const ERec& rc, const ERec& rp)
 {
-    const uint32_t ep = a.row_epoch[cur] << 4;
-    P4 r = philox4x32_10(cur, prev, 0, ep | kStreamAnchor, a.key0, a.key1);
-    uint32_t last = a.adj[rcur.off + pick(r.x0, rcur)];
+    const uint32_t ep = a.row_epoch[rc.v] << 4;
+    P4 r = philox4x32_10(rc.v, rp.v, 0, ep | kStreamAnchor, a.key0, a.key1);
+    uint32_t last = (uint32_t)pick32(r.x0, rc.deg);
     if (a.init == kInitWeight) {
-        float best = weight<kNode2Vec>(a, prev, rprev, last);
+        float best = weight<kNode2Vec>(a, rp, a.adj[rc.off + last]);
         for (uint32_t j = 1; j <= 20; j++) {
-            r = philox4x32_10(cur, prev, j, ep | kStreamAnchor, a.key0, a.key1);
-            const uint32_t cand = a.adj[rcur.off + pick(r.x0, rcur)];
-            const float w = weight<kNode2Vec>(a, prev, rprev, cand);
+            r = philox4x32_10(rc.v, rp.v, j, ep | kStreamAnchor, a.key0, a.key1);
+            const uint32_t cand = (uint32_t)pick32(r.x0, rc.deg);
+            const float w = weight<kNode2Vec>(a, rp, a.adj[rc.off + cand]);
             if (w > best) { best = w; last = cand; }
         }
     } else if (a.init == kInitBurnin) {
         for (uint32_t i = 0; i < 100; i++) {
-            r = philox4x32_10(cur, prev, i, ep | kStreamBurnin, a.key0, a.key1);
-            const uint32_t cand = a.adj[rcur.off + pick(r.x0, rcur)];
-            const float wn = weight<kNode2Vec>(a, prev, rprev, cand);
-            const float wl = weight<kNode2Vec>(a, prev, rprev, last);
+            r = philox4x32_10(rc.v, rp.v, i, ep | kStreamBurnin, a.key0, a.key1);
+            const uint32_t cand = (uint32_t)pick32(r.x0, rc.deg);
+            const float wn = weight<kNode2Vec>(a, rp, a.adj[rc.off + cand]);
+            const float wl = weight<kNode2Vec>(a, rp, a.adj[rc.off + last]);
             if (wl < wn || u01(r.x1, r.x2) <= (double)wn / (double)wl) last = cand;
         }
     }
@@ -90,42 +71,52 @@ __device__ uint32_t anchor_init(const WalkArgs& a, uint32_t cur, const VR& rcur,
 }
 
 // SamplerManager::find (copy, so the anchor stays frozen: libcuckoo find()
-// returns by value, cuckoohash_map.hh:596-609).  Lazily initialised; every
-// writer of a slot writes the same value (pure function of the slot's inputs).
-template <class VR>
-__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, uint32_t cur, const VR& rcur, uint32_t prev,
-                                               const VR& rprev)
+// returns by value, cuckoohash_map.hh:596-609).  The cache slot of state
+// (cur, prev) is prev's slot in cur's row; lazily initialised, and every writer
+// of a slot writes the same value (a pure function of the slot's inputs).
+__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const ERec& rc, const ERec& rp)
 {
-    const int64_t slot = row_find(a.adj, rcur, prev);
-    if (slot < 0) return anchor_init(a, cur, rcur, prev, rprev);
+    const int64_t slot = row_find(a.adj, rc, rp.v);
+    if (slot < 0) return anchor_init(a, rc, rp);
     uint32_t an = a.anchor[slot];
     if (an == kAnchorNone) {
-        an = anchor_init(a, cur, rcur, prev, rprev);
+        an = anchor_init(a, rc, rp);
         a.anchor[slot] = an;
     }
     return an;
 }
 
+__device__ __forceinline__ ERec load_rec(const ERec* p, uint64_t i)
+{
+    // one 16-B load: the next vertex and its row in the same cache line
+    const uint4 q = *reinterpret_cast<const uint4*>(p + i);
+    ERec r;
+    r.v = q.x; r.deg = q.y; r.off = ((uint64_t)q.w << 32) | q.z;
+    return r;
+}
+
 // ---------------------------------------------------------------------------
 // The walk kernel: generation (REWALK=false, wharfmh.h:275-326) and fused
 // rewalk-point scan + suffix re-walk (REWALK=true, wharfmh.h:519-537 + 761-859).
-// One lane per walk; lane li owns walk matrix column li.
+// One lane per walk; lane li owns walk matrix column li.  The walker carries
+// the edge record of its current vertex, so a step is ONE dependent 16-B
+// gather: erec[cur.off + pick] = {next vertex, next degree, next row offset}.
 // ---------------------------------------------------------------------------
-template <class VR, int MODEL, bool DET, bool REWALK>
+template <int MODEL, bool DET, bool REWALK>
 __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
 {
     const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t steps = 0, accepts = 0;
     if (li < a.W) {
-        const VR* __restrict__ vrec = reinterpret_cast<const VR*>(a.vrec);
-        const uint32_t* __restrict__ adj = a.adj;
+        const ERec* __restrict__ vrec = a.vrec;
+        const ERec* __restrict__ erec = a.erec;
         uint32_t* __restrict__ walks = a.walks;
         const uint64_t W = a.W;
         const uint64_t r = li / a.n_loc;
         const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
         const uint64_t wid = r * a.n + v;
 
-        uint32_t p = 0, cur = v, prev = v;
+        uint32_t p = 0, cur = v;
         bool go = true;
         if constexpr (REWALK) {
             // min position of any batch source in this walk, over the old corpus
@@ -137,54 +128,56 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
             }
             a.aff[li] = (uint8_t)p;
             go = p != kNoRewalk && !a.scan_only;
-            if (go && MODEL == kNode2Vec && !DET && p > 0) prev = walks[(uint64_t)(p - 1) * W + li];
         } else {
             walks[li] = v;
         }
         if (go) {
             const uint32_t ep = a.epoch << 4;
             const uint32_t wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
+            ERec rc = load_rec(vrec, cur);
+            ERec rp = rc;
             if constexpr (MODEL == kNode2Vec && !DET) {
-                if (p == 0) {
+                if (p > 0) {
+                    rp = load_rec(vrec, walks[(uint64_t)(p - 1) * W + li]);
+                } else if (rc.deg) {
                     // Node2Vec::initial_state: prev = random neighbour (node2vec.h:42-50)
-                    const VR rv = vrec[cur];
-                    if (rv.deg) {
-                        const P4 q = philox4x32_10(wlo, whi, 0, ep | kStreamPrev, a.key0, a.key1);
-                        prev = adj[rv.off + pick(q.x0, rv)];
-                    }
+                    const P4 q = philox4x32_10(wlo, whi, 0, ep | kStreamPrev, a.key0, a.key1);
+                    rp = load_rec(erec, rc.off + pick32(q.x0, rc.deg));
                 }
             }
             const uint64_t* __restrict__ rt = DET ? a.rtab + r * a.L : nullptr;
             uint32_t pos = p;
             for (; pos + 1 < a.L; pos++) {
-                const VR rc = vrec[cur];
                 if (rc.deg == 0) break;   // dead end: the walk stops (reference: lrand() % 0)
-                uint32_t nxt;
+                ERec nx;
                 if constexpr (DET) {
                     // Random(wid / n) restarted at the walk's first re-walked position
-                    const uint64_t x = rt[pos - p];
-                    if constexpr (sizeof(VR) == 8) nxt = adj[rc.off + umod64_32(x, (uint32_t)rc.deg)];
-                    else nxt = adj[rc.off + x % rc.deg];
+                    nx = load_rec(erec, rc.off + umod64_32(rt[pos - p], rc.deg));
                 } else {
                     const P4 q = philox4x32_10(wlo, whi, pos, ep | kStreamStep, a.key0, a.key1);
-                    const uint32_t c = adj[rc.off + pick(q.x0, rc)];
+                    const uint32_t ci = (uint32_t)pick32(q.x0, rc.deg);
+                    const ERec cand = load_rec(erec, rc.off + ci);
                     if constexpr (MODEL == kDeepWalk) {
-                        nxt = c;   // weights are all 1: sample() always accepts
+                        nx = cand;   // weights are all 1: sample() always accepts
                         accepts++;
                     } else {
-                        const VR rp = vrec[prev];
-                        const uint32_t an = anchor_get(a, cur, rc, prev, rp);
-                        const float wc = weight<MODEL>(a, prev, rp, c);
-                        const float wa = (an == c) ? wc : weight<MODEL>(a, prev, rp, an);
-                        const bool ok = (wa < wc) || (u01(q.x1, q.x2) <= (double)wc / (double)wa);
-                        nxt = ok ? c : an;
+                        const uint32_t ai = anchor_get(a, rc, rp);
+                        const float wc = weight<MODEL>(a, rp, cand.v);
+                        bool ok = true;
+                        if (ai != ci) {
+                            const ERec an = load_rec(erec, rc.off + ai);
+                            const float wa = an.v == cand.v ? wc : weight<MODEL>(a, rp, an.v);
+                            ok = (wa < wc) || (u01(q.x1, q.x2) <= (double)wc / (double)wa);
+                            if (!ok) nx = an;
+                        }
+                        if (ok) nx = cand;
                         accepts += ok;
                     }
                 }
-                walks[(uint64_t)(pos + 1) * W + li] = nxt;
+                walks[(uint64_t)(pos + 1) * W + li] = nx.v;
                 steps++;
-                prev = cur;
-                cur = nxt;
+                rp = rc;
+                rc = nx;
             }
             for (pos = pos + 1; pos < a.L; pos++) walks[(uint64_t)pos * W + li] = kSent;
         }
@@ -193,28 +186,19 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
     wave_add(a.counters + 1, accepts);
 }
 
-template <class VR>
-static void launch_walk_vr(const WalkArgs& a, bool rewalk, hipStream_t s)
+void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
 {
+    if (a.W == 0) return;
     const dim3 grid((unsigned)((a.W + 255) / 256)), block(256);
-    const bool det = a.det != 0;
-    const int model = a.model;
-#define WHARF_LAUNCH(M, D, R) hipLaunchKernelGGL((k_walk<VR, M, D, R>), grid, block, 0, s, a)
-    if (det) {
+#define WHARF_LAUNCH(M, D, R) hipLaunchKernelGGL((k_walk<M, D, R>), grid, block, 0, s, a)
+    if (a.det) {
         if (rewalk) WHARF_LAUNCH(kDeepWalk, true, true); else WHARF_LAUNCH(kDeepWalk, true, false);
-    } else if (model == kDeepWalk) {
+    } else if (a.model == kDeepWalk) {
         if (rewalk) WHARF_LAUNCH(kDeepWalk, false, true); else WHARF_LAUNCH(kDeepWalk, false, false);
     } else {
         if (rewalk) WHARF_LAUNCH(kNode2Vec, false, true); else WHARF_LAUNCH(kNode2Vec, false, false);
     }
 #undef WHARF_LAUNCH
-}
-
-void launch_walk(const WalkArgs& a, bool wide, bool rewalk, hipStream_t s)
-{
-    if (a.W == 0) return;
-    if (wide) launch_walk_vr<VRec64>(a, rewalk, s);
-    else launch_walk_vr<VRec32>(a, rewalk, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -286,22 +270,32 @@ __global__ void k_low32(const uint64_t* __restrict__ keys, uint64_t m, uint32_t*
         out[i] = (uint32_t)keys[i];
 }
 
-template <class VR>
-__global__ void k_vrec(const uint64_t* __restrict__ off, uint64_t n, VR* __restrict__ vrec)
+__global__ void k_vrec(const uint64_t* __restrict__ off, uint64_t n, ERec* __restrict__ vrec)
 {
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
-        VR r;
-        r.off = (decltype(r.off))off[v];
-        r.deg = (decltype(r.deg))(off[v + 1] - off[v]);
+        ERec r;
+        r.v = (uint32_t)v;
+        r.deg = (uint32_t)(off[v + 1] - off[v]);
+        r.off = off[v];
         vrec[v] = r;
     }
 }
 
-void launch_vrec(const uint64_t* off, uint64_t n, void* vrec, bool wide, hipStream_t s)
+// erec[e] = vrec[adj[e]]: every CSR slot carries its target's row
+__global__ void k_erec(const uint32_t* __restrict__ adj, uint64_t m, const ERec* __restrict__ vrec, ERec* __restrict__ erec)
 {
-    const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256 + 1, 65535);
-    if (wide) hipLaunchKernelGGL(k_vrec<VRec64>, g, 256, 0, s, off, n, (VRec64*)vrec);
-    else hipLaunchKernelGGL(k_vrec<VRec32>, g, 256, 0, s, off, n, (VRec32*)vrec);
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x)
+        erec[e] = vrec[adj[e]];
+}
+
+void launch_vrec(const uint64_t* off, uint64_t n, ERec* vrec, hipStream_t s)
+{
+    if (n) hipLaunchKernelGGL(k_vrec, grid_for(n, 256), 256, 0, s, off, n, vrec);
+}
+
+void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, hipStream_t s)
+{
+    if (m) hipLaunchKernelGGL(k_erec, grid_for(m, 256), 256, 0, s, adj, m, vrec, erec);
 }
 
 // Per batch edge (sorted, unique): does it change its source row?

@@ -166,26 +166,30 @@ class WharfMH:
     def generate_initial_random_walks(self) -> None:
         L.check(L.lib.wharf_generate(self._h), self._h, "generate_initial_random_walks")
 
-    def _update(self, fn, edges, sorted, remove_dups, apply_walk_updates) -> np.ndarray:
+    def _update(self, fn, edges, sorted, remove_dups, apply_walk_updates, out) -> np.ndarray:
         e = np.ascontiguousarray(np.asarray(edges, dtype=np.uint32).reshape(-1, 2))
         flags = (L.WHARF_SORTED if sorted else 0) | (L.WHARF_REMOVE_DUPS if remove_dups else 0) | \
                 (L.WHARF_APPLY_WALK_UPDATES if apply_walk_updates else 0)
-        out = np.zeros(max(self.number_of_walks, 1), dtype=np.uint32)
+        W = max(self.number_of_walks, 1)
+        buf = out if out is not None else np.empty(W, dtype=np.uint32)
+        if buf.dtype != np.uint32 or len(buf) < W or not buf.flags.c_contiguous:
+            raise ValueError("out must be a contiguous uint32 array with >= number_of_walks entries")
         cnt = C.c_uint64()
-        L.check(fn(self._h, len(e), _ptr(e), flags, _ptr(out), C.byref(cnt)), self._h, fn.__name__)
-        return out[: cnt.value].copy()
+        L.check(fn(self._h, len(e), _ptr(e), flags, _ptr(buf), C.byref(cnt)), self._h, fn.__name__)
+        return buf[: cnt.value]
 
     def insert_edges_batch(self, edges, sorted: bool = False, remove_dups: bool = False, nn: int | None = None,
-                           apply_walk_updates: bool = True, run_seq: bool = False) -> np.ndarray:
+                           apply_walk_updates: bool = True, run_seq: bool = False, out=None) -> np.ndarray:
         """wharfmh.h:439.  `edges`: (m, 2) (src, dst).  Returns the affected walk ids
-        (ascending).  `nn` and `run_seq` are CPU-sort/scheduling hints of the
-        reference and have no effect here; the caller's buffer is not modified."""
-        return self._update(L.lib.wharf_insert_edges, edges, sorted, remove_dups, apply_walk_updates)
+        (ascending; a view of `out` when given).  `nn` and `run_seq` are CPU
+        sort/scheduling hints of the reference and have no effect here; the
+        caller's buffer is not modified."""
+        return self._update(L.lib.wharf_insert_edges, edges, sorted, remove_dups, apply_walk_updates, out)
 
     def delete_edges_batch(self, edges, sorted: bool = False, remove_dups: bool = False, nn: int | None = None,
-                           apply_walk_updates: bool = True, run_seq: bool = False) -> np.ndarray:
+                           apply_walk_updates: bool = True, run_seq: bool = False, out=None) -> np.ndarray:
         """wharfmh.h:588."""
-        return self._update(L.lib.wharf_delete_edges, edges, sorted, remove_dups, apply_walk_updates)
+        return self._update(L.lib.wharf_delete_edges, edges, sorted, remove_dups, apply_walk_updates, out)
 
     def walk(self, walk_id: int) -> str:
         """WharfMH::walk (wharfmh.h:365): "v0 v1 ... " with a trailing space."""

@@ -21,6 +21,7 @@ for s in "$@"; do
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench18) step bench_s18 600 python bench.py --scale 18 --samples 7324270 --steps 3 --warmup 1 --cpu-baseline off ;;
     bench)  step bench 900 python bench.py ;;
+    benchq) step benchq 600 python bench.py --cpu-baseline off ;;
     prof)   step prof_gen 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_gen -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-baseline off ;;
     pmc)    step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 0 --rewalk-batches 0 --cpu-baseline off
             step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 0 --rewalk-batches 0 --cpu-baseline off ;;
