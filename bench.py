@@ -59,14 +59,8 @@ def parse():
 
 
 def balanced_shards(deg: np.ndarray, parts: int):
-    """contiguous start-vertex ranges with equal numbers of non-isolated vertices"""
-    act = np.cumsum(deg > 0)
-    total = int(act[-1]) if len(act) else 0
-    bounds = [0]
-    for k in range(1, parts):
-        bounds.append(int(np.searchsorted(act, (total * k) // parts, side="right")))
-    bounds.append(len(deg))
-    return [(bounds[i], bounds[i + 1]) for i in range(parts)]
+    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards as bs
+    return bs(deg, parts)
 
 
 def load_traffic(tag: str):
@@ -136,10 +130,17 @@ def main():
     import torch
 
     dist = None
+    # one process per GPU; more ranks than GPUs (a 1-GPU rehearsal) share devices round-robin
+    dev = local % max(torch.cuda.device_count(), 1)
+    backend = os.environ.get("WHARF_DIST_BACKEND", "nccl")   # gloo: rehearsal of the N>1 path on one GPU
+    comm_dev = "cpu" if backend == "gloo" else f"cuda:{dev}"
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     import dynamicgraphrepresentationlearning_amd as W
 
     n = 1 << args.scale
@@ -147,7 +148,7 @@ def main():
                         model=W.NODE2VEC if args.model == "node2vec" else W.DEEPWALK,
                         paramP=args.paramP, paramQ=args.paramQ, deterministic=args.det, seed=0x5EED)
     t0 = time.time()
-    g = W.WharfMH.from_rmat(n, args.samples, 2 * n, seed=args.seed, config=cfg, device=local)
+    g = W.WharfMH.from_rmat(n, args.samples, 2 * n, seed=args.seed, config=cfg, device=dev)
     off, adj = g.flatten_graph() if rank == 0 else (None, None)
     off_np = off if off is not None else g.flatten_graph()[0]
     deg = np.diff(off_np.astype(np.int64))
@@ -159,7 +160,7 @@ def main():
     def barrier():
         if dist:
             dist.barrier()
-        torch.cuda.synchronize(local)
+        torch.cuda.synchronize(dev)
 
     for i in range(args.warmup):
         g.generate_initial_random_walks()
@@ -176,7 +177,7 @@ def main():
     steps_local = st["steps"]
     steps_total, t_max = steps_local, elapsed
     if dist:
-        tt = torch.tensor([float(steps_local), elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([float(steps_local), elapsed], dtype=torch.float64, device=comm_dev)
         s = tt.clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         mx = tt.clone()
@@ -187,21 +188,38 @@ def main():
     bytes_per_step = BYTES_PER_STEP_DEEPWALK if args.model == "deepwalk" else None
     tag = f"gen_{args.model}_{'det' if args.det else 'mh'}_s{args.scale}"
 
-    # re-walk latency: 10k-edge batches (generate_batch_of_edges(5000, n, b, false, undirected))
+    # corpus reassembly for the downstream consumer: full-mesh all-gatherv over RCCL (not timed in `value`)
+    corpus = None
+    if dist:
+        from dynamicgraphrepresentationlearning_amd.distributed import allgatherv_corpus
+        shards = balanced_shards(deg, world)
+        loc = torch.empty((g.number_of_walks, args.length), dtype=torch.int32, device=f"cuda:{dev}")
+        g.export_walks_device(loc.data_ptr(), layout="walk")
+        loc = loc.to(comm_dev)
+        barrier()
+        t1 = time.perf_counter()
+        full = allgatherv_corpus(loc, shards, n, args.wpv)
+        barrier()
+        gms = (time.perf_counter() - t1) * 1e3
+        recv = full.numel() * 4 - loc.numel() * 4
+        corpus = {"ms": round(gms, 3), "bytes_received_per_rank": int(recv),
+                  "GBps_per_rank": round(recv / gms / 1e6, 1), "pattern": "batch_isend_irecv full mesh"}
+        del full, loc
+
     g.destroy()
 
     # configs[2]: soc-LiveJournal-sized streaming, 10k-edge insert batches
     # (memory-throughput-latency.cpp:126-134: generate_batch_of_edges(5000, n, seed=b, false, undirected))
     rewalk = None
     if args.rewalk_batches > 0:
-        gs = W.WharfMH.from_rmat(n, args.stream_samples, 2 * n, seed=args.seed + 1, config=cfg, device=local)
+        gs = W.WharfMH.from_rmat(n, args.stream_samples, 2 * n, seed=args.seed + 1, config=cfg, device=dev)
         gs.set_shard(lo, hi) if world == 1 else gs.set_shard(*balanced_shards(
             np.diff(gs.flatten_graph()[0].astype(np.int64)), world)[rank])
         gs.generate_initial_random_walks()
         out = np.empty(gs.number_of_walks, dtype=np.uint32)
         lat, aff, gu, wu, kern = [], [], [], [], []
         for b in range(args.rewalk_batches):
-            batch = W.generate_batch_of_edges(5000, n, b, False, False, device=local)
+            batch = W.generate_batch_of_edges(5000, n, b, False, False, device=dev)
             barrier()
             t1 = time.perf_counter()
             a = gs.insert_edges_batch(batch, remove_dups=True, out=out)
@@ -214,7 +232,7 @@ def main():
             kern.append(s2["last_walk_kernel_ms"])
         lat_all = lat
         if dist:
-            tl = torch.tensor(lat, dtype=torch.float64, device=f"cuda:{local}")
+            tl = torch.tensor(lat, dtype=torch.float64, device=comm_dev)
             dist.all_reduce(tl, op=dist.ReduceOp.MAX)
             lat_all = tl.tolist()
         rewalk = {"workload": f"configs[2] soc-LiveJournal-sized streaming: RMAT scale {args.scale}, "
@@ -257,6 +275,7 @@ def main():
                          "traffic": traffic, "bytes_per_step": bytes_per_step,
                          "avg_kernel_ms": round(avg_kernel_ms, 3)},
             "rewalk_latency_10k_batch": rewalk,
+            "corpus_allgatherv": corpus,
             "cpu_baseline": None,
         }
         if world == 1 and args.cpu_baseline != "off":

@@ -94,9 +94,9 @@ def test_errors_without_a_device_are_reported_not_crashed():
 
 
 def test_balanced_shards():
-    import bench
+    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards
     deg = np.array([0, 3, 0, 0, 1, 1, 2, 0, 5, 1], dtype=np.int64)
-    sh = bench.balanced_shards(deg, 3)
+    sh = balanced_shards(deg, 3)
     assert sh[0][0] == 0 and sh[-1][1] == len(deg)
     assert all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
     act = [int((deg[a:b] > 0).sum()) for a, b in sh]

@@ -346,3 +346,40 @@ def test_szudzik_device(W):
     ux, uy = W.szudzik64_unpair(z)
     np.testing.assert_array_equal(ux, x)
     np.testing.assert_array_equal(uy, y)
+
+
+@pytest.mark.parametrize("mode", ["det", "mh_deepwalk", "mh_node2vec"])
+def test_shards_reproduce_the_full_corpus(W, mode):
+    """Walks sharded by start-vertex range (the multi-GPU layout) are bit-identical
+    to the single-handle corpus, through generation and an insert/delete pair."""
+    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards, shard_walk_ids
+    n = 1 << 12
+    base = O.generate_batch_of_edges(60000, 2 * n, 8, False, False)
+    off, adj = O.csr_from_edges(n, base)
+    deg = np.diff(off.astype(np.int64))
+    kw = dict(walks_per_vertex=3, walk_length=30, seed=5, deterministic=(mode == "det"),
+              model=W.NODE2VEC if mode == "mh_node2vec" else W.DEEPWALK, paramP=0.5, paramQ=2.0)
+    full = W.WharfMH.from_csr(off, adj, config=W.WharfConfig(**kw))
+    full.generate_initial_random_walks()
+    b = O.generate_batch_of_edges(1500, n, 4, False, False)
+    fw0 = full.walks()
+    fa1 = full.insert_edges_batch(b, remove_dups=True).copy()
+    fw1 = full.walks()
+    fa2 = full.delete_edges_batch(b, remove_dups=True).copy()
+    fw2 = full.walks()
+    for lo, hi in balanced_shards(deg, 3):
+        g = W.WharfMH.from_csr(off, adj, config=W.WharfConfig(shard_lo=lo, shard_hi=hi, **kw))
+        ids = shard_walk_ids(n, 3, lo, hi)
+        np.testing.assert_array_equal(g.walk_ids(), ids)
+        g.generate_initial_random_walks()
+        np.testing.assert_array_equal(g.walks(), fw0[ids])
+        a1 = g.insert_edges_batch(b, remove_dups=True)
+        np.testing.assert_array_equal(np.sort(a1), np.intersect1d(fa1, ids))
+        np.testing.assert_array_equal(g.walks(), fw1[ids])
+        a2 = g.delete_edges_batch(b, remove_dups=True)
+        np.testing.assert_array_equal(np.sort(a2), np.intersect1d(fa2, ids))
+        np.testing.assert_array_equal(g.walks(), fw2[ids])
+        with pytest.raises(RuntimeError):
+            g.walk(int(np.setdiff1d(np.arange(3 * n), ids)[0]))   # not owned by this shard
+        g.destroy()
+    full.destroy()

@@ -1,0 +1,89 @@
+// Random-gather roof on MI355X: the ceiling the walk kernel is judged against.
+//
+//   hipcc --offload-arch=gfx950 -O3 tools/gather_roof.hip -o tools/gather_roof && tools/gather_roof [GiB]
+//
+// A table of 16-B records (size like the edge-record array of the com-orkut-sized
+// graph, 3.7 GB) is gathered at uniformly random slots, one lane per "walk",
+// 79 gathers per lane, 4-B coalesced store per gather (the walk kernel's shape):
+//   dep    next slot depends on the loaded record (pointer chasing, like a walk)
+//   indep  slots from a counter hash (no dependency: max memory-level parallelism)
+//   stream the same bytes read sequentially (HBM streaming ceiling)
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHK(x)                                                                   \
+    do {                                                                         \
+        hipError_t e = (x);                                                      \
+        if (e != hipSuccess) {                                                   \
+            std::printf("%s: %s\n", #x, hipGetErrorString(e));                   \
+            std::exit(1);                                                        \
+        }                                                                        \
+    } while (0)
+
+__device__ __forceinline__ uint32_t mix(uint32_t x)
+{
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+__global__ void k_init(uint4* t, uint64_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        t[i] = make_uint4(mix((uint32_t)i), mix((uint32_t)i ^ 0x9e3779b9u), (uint32_t)i, 0);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ t, uint64_t n, uint32_t* __restrict__ out,
+                                                uint64_t W, int L)
+{
+    const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= W) return;
+    uint32_t x = mix((uint32_t)li);
+    for (int p = 0; p < L; p++) {
+        uint64_t slot;
+        if (MODE == 0) slot = __umulhi(x, (uint32_t)n);                          // dep
+        else if (MODE == 1) slot = __umulhi(mix((uint32_t)(li * 131 + p)), (uint32_t)n);   // indep
+        else slot = (li + (uint64_t)p * W) % n;                                   // stream
+        const uint4 r = t[slot];
+        out[(uint64_t)p * W + li] = r.x;
+        x = MODE == 0 ? mix(r.y ^ x) : x + r.y;
+    }
+}
+
+int main(int argc, char** argv)
+{
+    const double gib = argc > 1 ? std::atof(argv[1]) : 3.48;
+    const uint64_t n = (uint64_t)(gib * (1ull << 30) / 16);
+    const uint64_t W = 41943040;
+    const int L = 79;
+    uint4* t;
+    uint32_t* out;
+    CHK(hipMalloc(&t, n * 16));
+    CHK(hipMalloc(&out, W * L * 4));
+    hipLaunchKernelGGL(k_init, 4096, 256, 0, 0, t, n);
+    CHK(hipDeviceSynchronize());
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    const char* names[3] = {"dep", "indep", "stream"};
+    for (int rep = 0; rep < 2; rep++)
+        for (int mode = 0; mode < 3; mode++) {
+            CHK(hipEventRecord(a));
+            if (mode == 0) hipLaunchKernelGGL(k_gather<0>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 1) hipLaunchKernelGGL(k_gather<1>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 2) hipLaunchKernelGGL(k_gather<2>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            CHK(hipEventRecord(b));
+            CHK(hipEventSynchronize(b));
+            float ms;
+            CHK(hipEventElapsedTime(&ms, a, b));
+            const double g = (double)W * L;
+            if (rep == 1)
+                std::printf("{\"mode\": \"%s\", \"table_GiB\": %.2f, \"ms\": %.3f, \"Ggathers_per_s\": %.2f, "
+                            "\"useful_GBps_16B\": %.1f}\n",
+                            names[mode], gib, ms, g / ms / 1e6, g * 20 / ms / 1e6);
+        }
+    return 0;
+}
