@@ -137,12 +137,12 @@ struct wharf_handle {
 
     void finish_graph()
     {
-        build_records();
         row_epoch.ensure(std::max<uint64_t>(n, 1) * 4);
         HIPCHK(hipMemsetAsync(row_epoch.p, 0, std::max<uint64_t>(n, 1) * 4, s));
+        build_records();
         if (anchors) {
-            anchor.ensure(std::max<uint64_t>(m, 1) * 4);
-            launch_fill_u32(anchor.as<uint32_t>(), m, kAnchorNone, s);
+            anchor.ensure(std::max<uint64_t>(m, 1) * 8);
+            launch_fill_u64(anchor.as<uint64_t>(), m, kAnchorNone64, s);
         }
         bitmap.ensure(((n + 31) / 32 + 1) * 4);
         sync();
@@ -163,7 +163,7 @@ struct wharf_handle {
     {
         vrec.ensure(std::max<uint64_t>(n, 1) * sizeof(ERec));
         erec.ensure(std::max<uint64_t>(m, 1) * sizeof(ERec));
-        launch_vrec(off.as<uint64_t>(), n, vrec.as<ERec>(), s);
+        launch_vrec(off.as<uint64_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
         launch_erec(adj.as<uint32_t>(), m, vrec.as<ERec>(), erec.as<ERec>(), s);
     }
 
@@ -174,8 +174,7 @@ struct wharf_handle {
         a.vrec = vrec.as<ERec>();
         a.erec = erec.as<ERec>();
         a.adj = adj.as<uint32_t>();
-        a.anchor = anchors ? anchor.as<uint32_t>() : nullptr;
-        a.row_epoch = row_epoch.as<uint32_t>();
+        a.anchor = anchors ? anchor.as<uint64_t>() : nullptr;
         a.walks = walks.as<uint32_t>();
         a.rtab = rtab.as<uint64_t>();
         a.bitmap = bitmap.as<uint32_t>();
@@ -391,18 +390,18 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->runs.ensure(k * sizeof(RunInfo));
         HIPCHK(hipMemsetAsync(h->bitmap.p, 0, ((h->n + 31) / 32 + 1) * 4, s));
         launch_run_info(bkeys, h->runstart.as<uint32_t>(), k, mb, h->off.as<uint64_t>(), h->runs.as<RunInfo>(),
-                        h->bitmap.as<uint32_t>(), h->anchors ? h->row_epoch.as<uint32_t>() : nullptr, h->epoch, s);
+                        h->bitmap.as<uint32_t>(), h->row_epoch.as<uint32_t>(), h->epoch, s);
         h->off2.ensure((h->n + 1) * 8);
         h->adj2.ensure(std::max<uint64_t>(m_new, 1) * 4);
-        if (h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 4);
+        if (h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8);
         launch_new_offsets(h->off.as<uint64_t>(), h->n, bkeys, mb, h->cf.as<uint32_t>(), insert, h->off2.as<uint64_t>(), s);
-        launch_move_edges(h->adj.as<uint32_t>(), h->anchors ? h->anchor.as<uint32_t>() : nullptr, h->m,
+        launch_move_edges(h->adj.as<uint32_t>(), h->anchors ? h->anchor.as<uint64_t>() : nullptr, h->m,
                           h->runs.as<RunInfo>(), k, bkeys, h->cf.as<uint32_t>(), h->off2.as<uint64_t>(), insert,
-                          h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint32_t>() : nullptr, m_new, s);
+                          h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint64_t>() : nullptr, m_new, s);
         if (insert)
             launch_place_new(bkeys, mb, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(), h->runstart.as<uint32_t>(), k,
                              h->runs.as<RunInfo>(), h->adj.as<uint32_t>(), h->off2.as<uint64_t>(),
-                             h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint32_t>() : nullptr, m_new, s);
+                             h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint64_t>() : nullptr, m_new, s);
         std::swap(h->off, h->off2);
         std::swap(h->adj, h->adj2);
         if (h->anchors) std::swap(h->anchor, h->anchor2);
@@ -825,7 +824,7 @@ int wharf_get_stats(const wharf_handle* h, wharf_stats* out)
     out->m = h->m;
     out->walks = h->W;
     out->hbm_bytes_walks = h->W * h->L * 4;
-    out->hbm_bytes_graph = (h->n + 1) * 8 + h->m * 4 + (h->n + h->m) * sizeof(ERec) + (h->anchors ? h->m * 4 : 0);
+    out->hbm_bytes_graph = (h->n + 1) * 8 + h->m * 4 + (h->n + h->m) * sizeof(ERec) + (h->anchors ? h->m * 8 : 0);
     return WHARF_OK;
 }
 

@@ -21,13 +21,42 @@ constexpr uint32_t kNoRewalk = 0xFFu;          // rewalk position "none"
 // Philox counter word 3 = (epoch << 4) | stream
 enum : uint32_t { kStreamStep = 0, kStreamAnchor = 1, kStreamBurnin = 2, kStreamPrev = 3 };
 
-// Row record: a vertex and its CSR row.  vrec[v] = {v, deg(v), off(v)};
+// Row record: a vertex and its CSR row.  vrec[v] = {v, deg(v), off(v), epoch(v)};
 // erec[e] = vrec[adj[e]], so a walk step reads its next vertex AND that
-// vertex's row with one aligned 16-B load.
+// vertex's row with one aligned 16-B load.  In memory the row offset (40 bits)
+// and the epoch of the row's last sampler reset (24 bits) share one word.
 struct alignas(16) ERec {
     uint32_t v, deg;
+    uint64_t oe;
+};
+struct Row {          // unpacked, in registers
+    uint32_t v, deg, epoch;
     uint64_t off;
 };
+constexpr uint64_t kOffBits = 40;
+constexpr uint64_t kOffMask = (1ull << kOffBits) - 1;
+constexpr uint64_t kAnchorNone64 = ~0ull;
+
+__host__ __device__ __forceinline__ ERec make_rec(uint32_t v, uint32_t deg, uint64_t off, uint32_t epoch)
+{
+    ERec r;
+    r.v = v;
+    r.deg = deg;
+    r.oe = (off & kOffMask) | ((uint64_t)epoch << kOffBits);
+    return r;
+}
+
+__device__ __forceinline__ Row load_rec(const ERec* p, uint64_t i)
+{
+    const uint4 q = *reinterpret_cast<const uint4*>(p + i);   // one global_load_dwordx4
+    const uint64_t oe = ((uint64_t)q.w << 32) | q.z;
+    Row r;
+    r.v = q.x;
+    r.deg = q.y;
+    r.off = oe & kOffMask;
+    r.epoch = (uint32_t)(oe >> kOffBits);
+    return r;
+}
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (Random123); 10 rounds, key bumped between rounds.

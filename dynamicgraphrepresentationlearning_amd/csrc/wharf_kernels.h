@@ -18,8 +18,7 @@ struct WalkArgs {
     const ERec* vrec;            // [n]: the row of each vertex
     const ERec* erec;            // [m]: per CSR slot, the target's row
     const uint32_t* adj;         // [m]: CSR targets (binary searches, anchor proposals)
-    uint32_t* anchor;            // MH anchors per CSR slot (node2vec MH), else null
-    const uint32_t* row_epoch;   // epoch of each row's last sampler reset (MH)
+    uint64_t* anchor;            // node2vec MH: per CSR slot (edge prev->cur) {anchor slot, epoch tag}
     uint32_t* walks;             // [L][W]
     const uint64_t* rtab;        // deterministic draws [wpv][L]
     const uint32_t* bitmap;      // batch sources (re-walk)
@@ -41,7 +40,7 @@ struct RunInfo {
 unsigned grid_for(uint64_t work, unsigned block);
 
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s);
-void launch_vrec(const uint64_t* off, uint64_t n, ERec* vrec, hipStream_t s);
+void launch_vrec(const uint64_t* off, uint64_t n, const uint32_t* row_epoch, ERec* vrec, hipStream_t s);
 void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, hipStream_t s);
 void launch_rmat_keys(const RmatParams& p, uint64_t M, int directed, uint64_t* keys, hipStream_t s);
 void launch_pairs_to_keys(const uint32_t* pairs, uint64_t m, uint64_t n, uint64_t* keys, unsigned long long* err, hipStream_t s);
@@ -56,12 +55,12 @@ void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t 
                      RunInfo* runs, uint32_t* bitmap, uint32_t* row_epoch, uint32_t epoch, hipStream_t s);
 void launch_new_offsets(const uint64_t* off, uint64_t n, const uint64_t* bkeys, uint64_t mb, const uint32_t* cf,
                         int insert, uint64_t* noff, hipStream_t s);
-void launch_move_edges(const uint32_t* adj, const uint32_t* anc, uint64_t m, const RunInfo* runs, uint64_t k,
+void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunInfo* runs, uint64_t k,
                        const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
-                       uint32_t* nanc, uint64_t cap, hipStream_t s);
+                       uint64_t* nanc, uint64_t cap, hipStream_t s);
 void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf,
                       const uint32_t* run_start, uint64_t k, const RunInfo* runs, const uint32_t* adj,
-                      const uint64_t* noff, uint32_t* nadj, uint32_t* nanc, uint64_t cap, hipStream_t s);
+                      const uint64_t* noff, uint32_t* nadj, uint64_t* nanc, uint64_t cap, hipStream_t s);
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s);
 void launch_gather_walk(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* out, hipStream_t s);
 void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t* len, hipStream_t s);
@@ -72,6 +71,7 @@ void launch_index_split(const uint64_t* skeys, uint64_t E, int kb, unsigned long
 void launch_li_to_wid(const uint64_t* li, uint64_t cnt, uint64_t n, uint64_t n_loc, uint64_t lo, uint32_t* out,
                       hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s);
+void launch_fill_u64(uint64_t* p, uint64_t cnt, uint64_t v, hipStream_t s);
 void launch_szudzik64(int op, uint64_t cnt, uint64_t* x, uint64_t* y, uint64_t* z, hipStream_t s);
 
 }  // namespace wharf

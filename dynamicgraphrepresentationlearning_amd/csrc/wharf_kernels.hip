@@ -22,7 +22,7 @@ __device__ __forceinline__ void wave_add(unsigned long long* dst, uint32_t v)
 }
 
 // std::binary_search over the ascending row (node2vec.h:112-119)
-__device__ __forceinline__ int64_t row_find(const uint32_t* __restrict__ adj, const ERec& r, uint32_t x)
+__device__ __forceinline__ int64_t row_find(const uint32_t* __restrict__ adj, const Row& r, uint32_t x)
 {
     uint64_t lo = r.off, hi = r.off + r.deg;
     while (lo < hi) {
@@ -34,7 +34,7 @@ __device__ __forceinline__ int64_t row_find(const uint32_t* __restrict__ adj, co
 
 // node2vec.h:74-88 (DeepWalk: deepwalk.h:67-70 returns 1); rprev = row of prev
 template <int MODEL>
-__device__ __forceinline__ float weight(const WalkArgs& a, const ERec& rprev, uint32_t c)
+__device__ __forceinline__ float weight(const WalkArgs& a, const Row& rprev, uint32_t c)
 {
     if constexpr (MODEL == kDeepWalk) return 1.0f;
     if (c == rprev.v) return a.inv_p;
@@ -43,11 +43,11 @@ __device__ __forceinline__ float weight(const WalkArgs& a, const ERec& rprev, ui
 }
 
 // MetropolisHastingsSampler::init (metropolis_hastings_sampler.h:69-108) with
-// proposals from the (cur, prev, row_epoch[cur]) Philox stream.  Returns the
-// anchor as a slot of cur's row.
-__device__ uint32_t anchor_init(const WalkArgs& a, const ERec& rc, const ERec& rp)
+// proposals from the (cur, prev, epoch of cur's row) Philox stream.  Returns
+// the anchor as a slot of cur's row.
+__device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp)
 {
-    const uint32_t ep = a.row_epoch[rc.v] << 4;
+    const uint32_t ep = rc.epoch << 4;
     P4 r = philox4x32_10(rc.v, rp.v, 0, ep | kStreamAnchor, a.key0, a.key1);
     uint32_t last = (uint32_t)pick32(r.x0, rc.deg);
     if (a.init == kInitWeight) {
@@ -70,37 +70,31 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const ERec& rc, const ERec& r
     return last;
 }
 
-// SamplerManager::find (copy, so the anchor stays frozen: libcuckoo find()
-// returns by value, cuckoohash_map.hh:596-609).  The cache slot of state
-// (cur, prev) is prev's slot in cur's row; lazily initialised, and every writer
-// of a slot writes the same value (a pure function of the slot's inputs).
-__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const ERec& rc, const ERec& rp)
+// SamplerManager::find (a copy, so the anchor stays frozen: libcuckoo find()
+// returns by value, cuckoohash_map.hh:596-609).  The anchor of state
+// (cur, prev) is cached on the edge prev->cur the walker just crossed (`ein`,
+// its global CSR slot, or -1), tagged with the epoch it was computed in; it
+// stays valid while neither row changed since (samplers of batch sources are
+// reset, wharfmh.h:504,539).  Every writer of an entry writes the same value,
+// a pure function of the current snapshot, so lazy races are benign and the
+// result does not depend on which walks (or which GPU) touched it first.
+__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, int64_t ein)
 {
-    const int64_t slot = row_find(a.adj, rc, rp.v);
-    if (slot < 0) return anchor_init(a, rc, rp);
-    uint32_t an = a.anchor[slot];
-    if (an == kAnchorNone) {
-        an = anchor_init(a, rc, rp);
-        a.anchor[slot] = an;
-    }
+    if (ein < 0) return anchor_init(a, rc, rp);
+    const uint64_t e = a.anchor[ein];
+    const uint32_t tag = (uint32_t)(e >> 32);
+    if (e != kAnchorNone64 && tag >= rc.epoch && tag >= rp.epoch) return (uint32_t)e;
+    const uint32_t an = anchor_init(a, rc, rp);
+    a.anchor[ein] = ((uint64_t)a.epoch << 32) | an;
     return an;
-}
-
-__device__ __forceinline__ ERec load_rec(const ERec* p, uint64_t i)
-{
-    // one 16-B load: the next vertex and its row in the same cache line
-    const uint4 q = *reinterpret_cast<const uint4*>(p + i);
-    ERec r;
-    r.v = q.x; r.deg = q.y; r.off = ((uint64_t)q.w << 32) | q.z;
-    return r;
 }
 
 // ---------------------------------------------------------------------------
 // The walk kernel: generation (REWALK=false, wharfmh.h:275-326) and fused
 // rewalk-point scan + suffix re-walk (REWALK=true, wharfmh.h:519-537 + 761-859).
 // One lane per walk; lane li owns walk matrix column li.  The walker carries
-// the edge record of its current vertex, so a step is ONE dependent 16-B
-// gather: erec[cur.off + pick] = {next vertex, next degree, next row offset}.
+// the record of its current vertex, so a step is ONE dependent 16-B gather:
+// erec[cur.off + pick] = {next vertex, its degree, row offset, row epoch}.
 // ---------------------------------------------------------------------------
 template <int MODEL, bool DET, bool REWALK>
 __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
@@ -134,8 +128,9 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
         if (go) {
             const uint32_t ep = a.epoch << 4;
             const uint32_t wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
-            ERec rc = load_rec(vrec, cur);
-            ERec rp = rc;
+            Row rc = load_rec(vrec, cur);
+            Row rp = rc;
+            int64_t ein = -1;   // slot of the edge prev -> cur (node2vec anchor cache key)
             if constexpr (MODEL == kNode2Vec && !DET) {
                 if (p > 0) {
                     rp = load_rec(vrec, walks[(uint64_t)(p - 1) * W + li]);
@@ -144,34 +139,36 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
                     const P4 q = philox4x32_10(wlo, whi, 0, ep | kStreamPrev, a.key0, a.key1);
                     rp = load_rec(erec, rc.off + pick32(q.x0, rc.deg));
                 }
+                if (rc.deg) ein = row_find(a.adj, rp, rc.v);
             }
             const uint64_t* __restrict__ rt = DET ? a.rtab + r * a.L : nullptr;
             uint32_t pos = p;
             for (; pos + 1 < a.L; pos++) {
                 if (rc.deg == 0) break;   // dead end: the walk stops (reference: lrand() % 0)
-                ERec nx;
+                Row nx;
                 if constexpr (DET) {
                     // Random(wid / n) restarted at the walk's first re-walked position
                     nx = load_rec(erec, rc.off + umod64_32(rt[pos - p], rc.deg));
                 } else {
                     const P4 q = philox4x32_10(wlo, whi, pos, ep | kStreamStep, a.key0, a.key1);
                     const uint32_t ci = (uint32_t)pick32(q.x0, rc.deg);
-                    const ERec cand = load_rec(erec, rc.off + ci);
+                    const Row cand = load_rec(erec, rc.off + ci);
                     if constexpr (MODEL == kDeepWalk) {
                         nx = cand;   // weights are all 1: sample() always accepts
                         accepts++;
                     } else {
-                        const uint32_t ai = anchor_get(a, rc, rp);
+                        const uint32_t ai = anchor_get(a, rc, rp, ein);
                         const float wc = weight<MODEL>(a, rp, cand.v);
                         bool ok = true;
                         if (ai != ci) {
-                            const ERec an = load_rec(erec, rc.off + ai);
-                            const float wa = an.v == cand.v ? wc : weight<MODEL>(a, rp, an.v);
+                            const Row an = load_rec(erec, rc.off + ai);
+                            const float wa = weight<MODEL>(a, rp, an.v);
                             ok = (wa < wc) || (u01(q.x1, q.x2) <= (double)wc / (double)wa);
                             if (!ok) nx = an;
                         }
                         if (ok) nx = cand;
                         accepts += ok;
+                        ein = (int64_t)(rc.off + (ok ? ci : ai));
                     }
                 }
                 walks[(uint64_t)(pos + 1) * W + li] = nx.v;
@@ -270,15 +267,11 @@ __global__ void k_low32(const uint64_t* __restrict__ keys, uint64_t m, uint32_t*
         out[i] = (uint32_t)keys[i];
 }
 
-__global__ void k_vrec(const uint64_t* __restrict__ off, uint64_t n, ERec* __restrict__ vrec)
+__global__ void k_vrec(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ row_epoch,
+                       ERec* __restrict__ vrec)
 {
-    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
-        ERec r;
-        r.v = (uint32_t)v;
-        r.deg = (uint32_t)(off[v + 1] - off[v]);
-        r.off = off[v];
-        vrec[v] = r;
-    }
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
+        vrec[v] = make_rec((uint32_t)v, (uint32_t)(off[v + 1] - off[v]), off[v], row_epoch ? row_epoch[v] : 0u);
 }
 
 // erec[e] = vrec[adj[e]]: every CSR slot carries its target's row
@@ -288,9 +281,9 @@ __global__ void k_erec(const uint32_t* __restrict__ adj, uint64_t m, const ERec*
         erec[e] = vrec[adj[e]];
 }
 
-void launch_vrec(const uint64_t* off, uint64_t n, ERec* vrec, hipStream_t s)
+void launch_vrec(const uint64_t* off, uint64_t n, const uint32_t* row_epoch, ERec* vrec, hipStream_t s)
 {
-    if (n) hipLaunchKernelGGL(k_vrec, grid_for(n, 256), 256, 0, s, off, n, vrec);
+    if (n) hipLaunchKernelGGL(k_vrec, grid_for(n, 256), 256, 0, s, off, n, row_epoch, vrec);
 }
 
 void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, hipStream_t s)
@@ -358,10 +351,10 @@ __global__ void k_new_offsets(const uint64_t* __restrict__ off, uint64_t n, cons
 }
 
 // Move every old edge to its slot in the new CSR (one coalesced streaming pass).
-__global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint32_t* __restrict__ anc, uint64_t m,
+__global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* __restrict__ anc, uint64_t m,
                              const RunInfo* __restrict__ runs, uint64_t k, const uint64_t* __restrict__ bkeys,
                              const uint32_t* __restrict__ cf, const uint64_t* __restrict__ noff, int insert,
-                             uint32_t* __restrict__ nadj, uint32_t* __restrict__ nanc, uint64_t cap)
+                             uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc, uint64_t cap)
 {
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
         // last source run whose row starts at or before e
@@ -389,7 +382,7 @@ __global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint32_t* _
             const uint64_t np = noff[ri.src] + (e - ri.off) + (insert ? before : -(int64_t)before);
             if (np >= cap) continue;   // never taken for a consistent CSR; keeps a bad input in bounds
             nadj[np] = x;
-            if (nanc) nanc[np] = kAnchorNone;
+            if (nanc) nanc[np] = kAnchorNone64;
         } else {
             const uint64_t shift = cf[ri.re];
             const uint64_t np = insert ? e + shift : e - shift;
@@ -404,7 +397,7 @@ __global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint32_t* _
 __global__ void k_place_new(const uint64_t* __restrict__ bkeys, uint64_t mb, const uint32_t* __restrict__ chg,
                             const uint32_t* __restrict__ cf, const uint32_t* __restrict__ run_start, uint64_t k,
                             const RunInfo* __restrict__ runs, const uint32_t* __restrict__ adj,
-                            const uint64_t* __restrict__ noff, uint32_t* __restrict__ nadj, uint32_t* __restrict__ nanc,
+                            const uint64_t* __restrict__ noff, uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc,
                             uint64_t cap)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mb; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -424,7 +417,7 @@ __global__ void k_place_new(const uint64_t* __restrict__ bkeys, uint64_t mb, con
         const uint64_t np = noff[ri.src] + (cf[i] - cf[ri.rs]) + (b - ri.off);
         if (np >= cap) continue;
         nadj[np] = d;
-        if (nanc) nanc[np] = kAnchorNone;
+        if (nanc) nanc[np] = kAnchorNone64;
     }
 }
 
@@ -509,6 +502,12 @@ __global__ void k_li_to_wid(const uint64_t* __restrict__ li, uint64_t cnt, uint6
     }
 }
 
+__global__ void k_fill_u64(uint64_t* __restrict__ p, uint64_t cnt, uint64_t v)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+
 __global__ void k_fill_u32(uint32_t* __restrict__ p, uint64_t cnt, uint32_t v)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x)
@@ -567,13 +566,13 @@ void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t 
 void launch_new_offsets(const uint64_t* off, uint64_t n, const uint64_t* bkeys, uint64_t mb, const uint32_t* cf, int insert,
                         uint64_t* noff, hipStream_t s)
 { hipLaunchKernelGGL(k_new_offsets, grid_for(n + 1, 256), 256, 0, s, off, n, bkeys, mb, cf, insert, noff); }
-void launch_move_edges(const uint32_t* adj, const uint32_t* anc, uint64_t m, const RunInfo* runs, uint64_t k,
+void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunInfo* runs, uint64_t k,
                        const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
-                       uint32_t* nanc, uint64_t cap, hipStream_t s)
+                       uint64_t* nanc, uint64_t cap, hipStream_t s)
 { if (m) hipLaunchKernelGGL(k_move_edges, grid_for(m, 256), 256, 0, s, adj, anc, m, runs, k, bkeys, cf, noff, insert, nadj, nanc, cap); }
 void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf, const uint32_t* run_start,
                       uint64_t k, const RunInfo* runs, const uint32_t* adj, const uint64_t* noff, uint32_t* nadj,
-                      uint32_t* nanc, uint64_t cap, hipStream_t s)
+                      uint64_t* nanc, uint64_t cap, hipStream_t s)
 { hipLaunchKernelGGL(k_place_new, grid_for(mb, 256), 256, 0, s, bkeys, mb, chg, cf, run_start, k, runs, adj, noff, nadj, nanc, cap); }
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s)
 {
@@ -592,6 +591,8 @@ void launch_index_split(const uint64_t* skeys, uint64_t E, int kb, unsigned long
 { hipLaunchKernelGGL(k_index_split, grid_for(E, 256), 256, 0, s, skeys, E, kb, counts, keys); }
 void launch_li_to_wid(const uint64_t* li, uint64_t cnt, uint64_t n, uint64_t n_loc, uint64_t lo, uint32_t* out, hipStream_t s)
 { if (cnt) hipLaunchKernelGGL(k_li_to_wid, grid_for(cnt, 256), 256, 0, s, li, cnt, n, n_loc, lo, out); }
+void launch_fill_u64(uint64_t* p, uint64_t cnt, uint64_t v, hipStream_t s)
+{ if (cnt) hipLaunchKernelGGL(k_fill_u64, grid_for(cnt, 256), 256, 0, s, p, cnt, v); }
 void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s)
 { if (cnt) hipLaunchKernelGGL(k_fill_u32, grid_for(cnt, 256), 256, 0, s, p, cnt, v); }
 void launch_szudzik64(int op, uint64_t cnt, uint64_t* x, uint64_t* y, uint64_t* z, hipStream_t s)

@@ -200,13 +200,13 @@ void wo_szudzik64_unpair(uint64_t z, uint64_t* x, uint64_t* y)
 /* ------------------------------------------------------------------------ */
 /* Engine                                                                     */
 /* ------------------------------------------------------------------------ */
-#define ANCHOR_NONE 0xFFFFFFFFu
+#define ANCHOR_NONE UINT64_C(0xFFFFFFFFFFFFFFFF)
 
 struct wo_engine {
     uint64_t n, m;
     uint64_t* off;        /* n+1 */
     uint32_t* adj;        /* m   */
-    uint32_t* anchor;     /* m   : frozen MH anchor per (cur, slot of prev) */
+    uint64_t* anchor;     /* m   : per edge slot (prev -> cur): frozen anchor slot | epoch tag << 32 */
     uint32_t* row_epoch;  /* n   : epoch of last sampler reset of the row */
     uint32_t wpv, L;
     int model, init, det;
@@ -252,43 +252,47 @@ static inline double u01(uint32_t hi, uint32_t lo) { return (double)((((uint64_t
 enum { ST_STEP = 0, ST_ANCHOR = 1, ST_BURNIN = 2, ST_PREV = 3 };
 
 /* metropolis_hastings_sampler.h:69-108, with the proposals drawn from the
- * counter-based stream of (cur, prev, row_epoch[cur]). */
+ * counter-based stream of (cur, prev, row_epoch[cur]).  Returns a slot of
+ * cur's row. */
 static uint32_t anchor_init(const wo_engine* e, uint32_t cur, uint32_t prev)
 {
-    uint64_t d = deg_of(e, cur);
+    uint64_t d = deg_of(e, cur), o = e->off[cur];
     uint32_t ep = e->row_epoch[cur] << 4;
     uint32_t r[4];
     philox_draw(e, cur, prev, 0, ep | ST_ANCHOR, r);
-    uint32_t last = e->adj[e->off[cur] + pick(r[0], d)];
+    uint32_t last = (uint32_t)pick(r[0], d);
     if (e->init == WO_INIT_WEIGHT) {
-        float best_w = weight(e, prev, last);
+        float best_w = weight(e, prev, e->adj[o + last]);
         for (uint32_t j = 1; j <= 20; j++) {
             philox_draw(e, cur, prev, j, ep | ST_ANCHOR, r);
-            uint32_t cand = e->adj[e->off[cur] + pick(r[0], d)];
-            float w = weight(e, prev, cand);
+            uint32_t cand = (uint32_t)pick(r[0], d);
+            float w = weight(e, prev, e->adj[o + cand]);
             if (w > best_w) { best_w = w; last = cand; }
         }
     } else if (e->init == WO_INIT_BURNIN) {
         for (uint32_t i = 0; i < 100; i++) {
             philox_draw(e, cur, prev, i, ep | ST_BURNIN, r);
-            uint32_t cand = e->adj[e->off[cur] + pick(r[0], d)];
-            float wn = weight(e, prev, cand), wl = weight(e, prev, last);
+            uint32_t cand = (uint32_t)pick(r[0], d);
+            float wn = weight(e, prev, e->adj[o + cand]), wl = weight(e, prev, e->adj[o + last]);
             if (wl < wn || u01(r[1], r[2]) <= (double)wn / (double)wl) last = cand;
         }
     }
     return last;
 }
 
-static uint32_t anchor_get(wo_engine* e, uint32_t cur, uint32_t prev)
+/* SamplerManager::find returns a copy (libcuckoo find(), cuckoohash_map.hh:596-609),
+ * so a state's anchor stays frozen.  Cached on the edge prev -> cur (`ein`,
+ * its CSR slot, or -1) with the epoch it was computed in; valid while neither
+ * row was reset since (samplers of batch sources are reset, wharfmh.h:504,539). */
+static uint32_t anchor_get(wo_engine* e, uint32_t cur, uint32_t prev, int64_t ein)
 {
-    int64_t slot = row_find(e, cur, prev);
-    if (slot < 0) return anchor_init(e, cur, prev);
-    uint32_t a = __atomic_load_n(&e->anchor[slot], __ATOMIC_RELAXED);
-    if (a == ANCHOR_NONE) {
-        a = anchor_init(e, cur, prev);
-        __atomic_store_n(&e->anchor[slot], a, __ATOMIC_RELAXED);
-    }
-    return a;
+    if (ein < 0) return anchor_init(e, cur, prev);
+    uint64_t a = __atomic_load_n(&e->anchor[ein], __ATOMIC_RELAXED);
+    uint32_t tag = (uint32_t)(a >> 32);
+    if (a != ANCHOR_NONE && tag >= e->row_epoch[cur] && tag >= e->row_epoch[prev]) return (uint32_t)a;
+    uint32_t s = anchor_init(e, cur, prev);
+    __atomic_store_n(&e->anchor[ein], ((uint64_t)e->epoch << 32) | s, __ATOMIC_RELAXED);
+    return s;
 }
 
 /* One walk from (v at position p) to the end of the walk.
@@ -306,6 +310,7 @@ static void walk_from(wo_engine* e, uint64_t wid, uint32_t v, uint32_t p, uint32
     w[p] = v;
     uint32_t cur = v;
     uint32_t ep = e->epoch << 4;
+    int64_t ein = (e->model == WO_NODE2VEC && !e->det && deg_of(e, v)) ? row_find(e, prev, cur) : -1;
     for (uint32_t pos = p; pos + 1 < e->L; pos++) {
         uint64_t d = deg_of(e, cur);
         if (d == 0) { for (uint32_t k = pos + 1; k < e->L; k++) w[k] = WO_SENT; return; }
@@ -315,16 +320,19 @@ static void walk_from(wo_engine* e, uint64_t wid, uint32_t v, uint32_t p, uint32
         } else {
             uint32_t r[4];
             philox_draw(e, (uint32_t)wid, (uint32_t)(wid >> 32), pos, ep | ST_STEP, r);
-            uint32_t c = e->adj[e->off[cur] + pick(r[0], d)];
+            uint32_t ci = (uint32_t)pick(r[0], d);
+            uint32_t c = e->adj[e->off[cur] + ci];
             if (e->model == WO_DEEPWALK) {
                 nxt = c;
                 (*acc)++;
             } else {
-                uint32_t a = anchor_get(e, cur, prev);
+                uint32_t ai = anchor_get(e, cur, prev, ein);
+                uint32_t a = e->adj[e->off[cur] + ai];
                 float wc = weight(e, prev, c), wa = weight(e, prev, a);
                 int ok = (wa < wc) || (u01(r[1], r[2]) <= (double)wc / (double)wa);
                 nxt = ok ? c : a;
                 *acc += ok;
+                ein = (int64_t)(e->off[cur] + (ok ? ci : ai));
             }
         }
         (*steps)++;
@@ -353,8 +361,8 @@ wo_engine* wo_create(uint64_t n, uint64_t m, const uint64_t* off, const uint32_t
     memcpy(e->off, off, (n + 1) * 8);
     e->adj = (uint32_t*)malloc((m ? m : 1) * 4);
     if (m) memcpy(e->adj, adj, m * 4);
-    e->anchor = (uint32_t*)malloc((m ? m : 1) * 4);
-    memset(e->anchor, 0xFF, (m ? m : 1) * 4);
+    e->anchor = (uint64_t*)malloc((m ? m : 1) * 8);
+    memset(e->anchor, 0xFF, (m ? m : 1) * 8);
     e->row_epoch = (uint32_t*)calloc(n ? n : 1, 4);
     e->wpv = wpv; e->L = L; e->model = model; e->init = init; e->det = deterministic;
     e->p = p; e->q = q; e->seed = seed;
@@ -448,7 +456,7 @@ uint64_t wo_update(wo_engine* e, int insert, uint64_t m, const uint32_t* pairs_i
     uint64_t* noff = (uint64_t*)malloc((e->n + 1) * 8);
     uint64_t cap = e->m + (insert ? m : 0);
     uint32_t* nadj = (uint32_t*)malloc((cap ? cap : 1) * 4);
-    uint32_t* nanc = (uint32_t*)malloc((cap ? cap : 1) * 4);
+    uint64_t* nanc = (uint64_t*)malloc((cap ? cap : 1) * 8);
     uint64_t bi = 0, o = 0;
     noff[0] = 0;
     for (uint64_t v = 0; v < e->n; v++) {
@@ -458,7 +466,7 @@ uint64_t wo_update(wo_engine* e, int insert, uint64_t m, const uint32_t* pairs_i
         uint64_t b1 = bi;
         if (b0 == b1) {
             memcpy(nadj + o, e->adj + a0, (a1 - a0) * 4);
-            memcpy(nanc + o, e->anchor + a0, (a1 - a0) * 4);
+            memcpy(nanc + o, e->anchor + a0, (a1 - a0) * 8);
             o += a1 - a0;
         } else if (insert) {
             uint64_t i = a0, j = b0;
