@@ -84,7 +84,8 @@ struct wharf_handle {
     uint32_t L = 0, wpv = 0;
     bool anchors = false, has_walks = false;
     uint32_t epoch = 0;
-    DevBuf off, adj, vrec, erec, anchor, row_epoch, off2, adj2, anchor2;
+    DevBuf off, adj, vrec, erec, anchor, row_epoch, off2, adj2, anchor2, ehash;
+    uint64_t ehash_mask = 0;
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
     DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, count, pairs, sel;
     wharf_stats st{};
@@ -158,13 +159,22 @@ struct wharf_handle {
         has_walks = false;
     }
 
-    // vertex rows and per-slot edge records (one 16-B gather per walk step)
+    // vertex rows and per-slot edge records (one 16-B gather per walk step);
+    // node2vec MH also gets the edge hash set for has_edge
     void build_records()
     {
         vrec.ensure(std::max<uint64_t>(n, 1) * sizeof(ERec));
         erec.ensure(std::max<uint64_t>(m, 1) * sizeof(ERec));
         launch_vrec(off.as<uint64_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
         launch_erec(adj.as<uint32_t>(), m, vrec.as<ERec>(), erec.as<ERec>(), s);
+        if (anchors) {
+            uint64_t cap = 64;
+            while (cap < 2 * m) cap <<= 1;   // load factor <= 1/2
+            ehash.ensure(cap * 8);
+            ehash_mask = cap - 1;
+            launch_fill_u64(ehash.as<uint64_t>(), cap, kEmptyKey, s);
+            launch_edge_hash_build(off.as<uint64_t>(), n, adj.as<uint32_t>(), ehash.as<uint64_t>(), ehash_mask, s);
+        }
     }
 
     WalkArgs walk_args()
@@ -175,6 +185,8 @@ struct wharf_handle {
         a.erec = erec.as<ERec>();
         a.adj = adj.as<uint32_t>();
         a.anchor = anchors ? anchor.as<uint64_t>() : nullptr;
+        a.ehash = anchors ? ehash.as<uint64_t>() : nullptr;
+        a.ehash_mask = ehash_mask;
         a.walks = walks.as<uint32_t>();
         a.rtab = rtab.as<uint64_t>();
         a.bitmap = bitmap.as<uint32_t>();
@@ -286,7 +298,7 @@ void free_handle(wharf_handle* h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->s) (void)hipStreamSynchronize(h->s);
-    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->anchor, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
+    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->ehash, &h->anchor, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
                       &h->aff, &h->rtab, &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags,
                       &h->chg, &h->cf, &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel})
         b->release();

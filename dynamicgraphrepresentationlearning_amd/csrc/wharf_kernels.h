@@ -18,7 +18,9 @@ struct WalkArgs {
     const ERec* vrec;            // [n]: the row of each vertex
     const ERec* erec;            // [m]: per CSR slot, the target's row
     const uint32_t* adj;         // [m]: CSR targets (binary searches, anchor proposals)
-    uint64_t* anchor;            // node2vec MH: per CSR slot (edge prev->cur) {anchor slot, epoch tag}
+    uint64_t* anchor;            // node2vec MH: per CSR slot (edge prev->cur) {anchor slot, epoch tag, class}
+    const uint64_t* ehash;       // node2vec: edge hash set (u << 32 | v), or null -> binary search
+    uint64_t ehash_mask;         // capacity - 1 (power of two)
     uint32_t* walks;             // [L][W]
     const uint64_t* rtab;        // deterministic draws [wpv][L]
     const uint32_t* bitmap;      // batch sources (re-walk)
@@ -72,6 +74,8 @@ void launch_li_to_wid(const uint64_t* li, uint64_t cnt, uint64_t n, uint64_t n_l
                       hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s);
 void launch_fill_u64(uint64_t* p, uint64_t cnt, uint64_t v, hipStream_t s);
+void launch_edge_hash_build(const uint64_t* off, uint64_t n, const uint32_t* adj, uint64_t* table, uint64_t mask,
+                            hipStream_t s);
 void launch_szudzik64(int op, uint64_t cnt, uint64_t* x, uint64_t* y, uint64_t* z, hipStream_t s);
 
 }  // namespace wharf

@@ -32,14 +32,53 @@ __device__ __forceinline__ int64_t row_find(const uint32_t* __restrict__ adj, co
     return (lo < r.off + r.deg && adj[lo] == x) ? (int64_t)lo : -1;
 }
 
-// node2vec.h:74-88 (DeepWalk: deepwalk.h:67-70 returns 1); rprev = row of prev
+// Edge set of the snapshot: open addressing over 64-bit keys (u << 32 | v),
+// 4-key (32-B) buckets, load <= 1/2.  One bucket read answers has_edge in
+// almost every case, instead of the log2(deg) dependent probes of
+// std::binary_search (node2vec.h:112-119).
+__device__ __forceinline__ uint64_t edge_hash(uint64_t k)
+{
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+__device__ __forceinline__ bool has_edge(const WalkArgs& a, const Row& rprev, uint32_t c)
+{
+    if (!a.ehash) return row_find(a.adj, rprev, c) >= 0;
+    const uint64_t key = ((uint64_t)rprev.v << 32) | c;
+    uint64_t b = (edge_hash(key) & a.ehash_mask) & ~3ull;
+    for (;;) {
+        const ulonglong2 q0 = *reinterpret_cast<const ulonglong2*>(a.ehash + b);
+        const ulonglong2 q1 = *reinterpret_cast<const ulonglong2*>(a.ehash + b + 2);
+        if (q0.x == key || q0.y == key || q1.x == key || q1.y == key) return true;
+        if (q0.x == kEmptyKey || q0.y == kEmptyKey || q1.x == kEmptyKey || q1.y == kEmptyKey) return false;
+        b = (b + 4) & a.ehash_mask;
+    }
+}
+
+// node2vec.h:74-88 (DeepWalk: deepwalk.h:67-70 returns 1); rprev = row of prev.
+// Weight class: 0 -> 1/p (return), 1 -> 1 (triangle), 2 -> 1/q (outward).
+template <int MODEL>
+__device__ __forceinline__ uint32_t weight_class(const WalkArgs& a, const Row& rprev, uint32_t c)
+{
+    if constexpr (MODEL == kDeepWalk) return 1;
+    if (c == rprev.v) return 0;
+    return has_edge(a, rprev, c) ? 1 : 2;
+}
+
+__device__ __forceinline__ float class_weight(const WalkArgs& a, uint32_t cls)
+{
+    return cls == 0 ? a.inv_p : (cls == 1 ? 1.0f : a.inv_q);
+}
+
 template <int MODEL>
 __device__ __forceinline__ float weight(const WalkArgs& a, const Row& rprev, uint32_t c)
 {
-    if constexpr (MODEL == kDeepWalk) return 1.0f;
-    if (c == rprev.v) return a.inv_p;
-    if (row_find(a.adj, rprev, c) >= 0) return 1.0f;
-    return a.inv_q;
+    return class_weight(a, weight_class<MODEL>(a, rprev, c));
 }
 
 // MetropolisHastingsSampler::init (metropolis_hastings_sampler.h:69-108) with
@@ -78,14 +117,23 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp)
 // reset, wharfmh.h:504,539).  Every writer of an entry writes the same value,
 // a pure function of the current snapshot, so lazy races are benign and the
 // result does not depend on which walks (or which GPU) touched it first.
-__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, int64_t ein)
+// The entry also keeps the anchor's weight class (it depends only on (prev,
+// anchor) and prev's row, which the tag covers), so an accepted step needs one
+// has_edge, not two.  Entry = slot | tag << 32 | class << 62.
+__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, int64_t ein,
+                                               uint32_t& cls)
 {
-    if (ein < 0) return anchor_init(a, rc, rp);
-    const uint64_t e = a.anchor[ein];
-    const uint32_t tag = (uint32_t)(e >> 32);
-    if (e != kAnchorNone64 && tag >= rc.epoch && tag >= rp.epoch) return (uint32_t)e;
+    if (ein >= 0) {
+        const uint64_t e = a.anchor[ein];
+        const uint32_t tag = (uint32_t)(e >> 32) & 0x3FFFFFFFu;
+        if (e != kAnchorNone64 && tag >= rc.epoch && tag >= rp.epoch) {
+            cls = (uint32_t)(e >> 62);
+            return (uint32_t)e;
+        }
+    }
     const uint32_t an = anchor_init(a, rc, rp);
-    a.anchor[ein] = ((uint64_t)a.epoch << 32) | an;
+    cls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + an]);
+    if (ein >= 0) a.anchor[ein] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     return an;
 }
 
@@ -157,16 +205,15 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
                         nx = cand;   // weights are all 1: sample() always accepts
                         accepts++;
                     } else {
-                        const uint32_t ai = anchor_get(a, rc, rp, ein);
-                        const float wc = weight<MODEL>(a, rp, cand.v);
-                        bool ok = true;
+                        uint32_t acls;
+                        const uint32_t ai = anchor_get(a, rc, rp, ein, acls);
+                        bool ok = true;   // proposing the anchor itself is always accepted
                         if (ai != ci) {
-                            const Row an = load_rec(erec, rc.off + ai);
-                            const float wa = weight<MODEL>(a, rp, an.v);
+                            const float wc = weight<MODEL>(a, rp, cand.v);
+                            const float wa = class_weight(a, acls);
                             ok = (wa < wc) || (u01(q.x1, q.x2) <= (double)wc / (double)wa);
-                            if (!ok) nx = an;
                         }
-                        if (ok) nx = cand;
+                        nx = ok ? cand : load_rec(erec, rc.off + ai);
                         accepts += ok;
                         ein = (int64_t)(rc.off + (ok ? ci : ai));
                     }
@@ -219,6 +266,33 @@ __global__ void k_pairs_to_keys(const uint32_t* __restrict__ pairs, uint64_t m, 
         if (s >= n || d >= n) atomicOr(err, 1ull);
         keys[i] = ((uint64_t)s << 32) | d;
     }
+}
+
+// insert every (u, v) of the CSR into the edge hash set (4-key buckets, linear probing)
+__global__ void k_edge_hash_build(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ adj,
+                                  unsigned long long* __restrict__ table, uint64_t mask)
+{
+    const uint64_t v0 = (uint64_t)blockIdx.x * 64;
+    for (uint64_t u = v0 + threadIdx.x / 64; u < min(v0 + 64, n); u += blockDim.x / 64) {
+        const uint64_t b0 = off[u], e0 = off[u + 1];
+        for (uint64_t j = b0 + (threadIdx.x & 63); j < e0; j += 64) {
+            const unsigned long long key = (u << 32) | adj[j];
+            uint64_t b = (edge_hash(key) & mask) & ~3ull;
+            for (bool done = false; !done; b = (b + 4) & mask) {
+                for (int k = 0; k < 4 && !done; k++) {
+                    const unsigned long long old = atomicCAS(table + b + k, (unsigned long long)kEmptyKey, key);
+                    done = old == kEmptyKey || old == key;
+                }
+            }
+        }
+    }
+}
+
+void launch_edge_hash_build(const uint64_t* off, uint64_t n, const uint32_t* adj, uint64_t* table, uint64_t mask,
+                            hipStream_t s)
+{
+    if (n) hipLaunchKernelGGL(k_edge_hash_build, (unsigned)((n + 63) / 64), 256, 0, s, off, n, adj,
+                              (unsigned long long*)table, mask);
 }
 
 __global__ void k_csr_to_keys(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ tgt,
