@@ -15,10 +15,12 @@ from .wharfmh import (  # noqa: F401
     WharfConfig,
     WharfMH,
     generate_batch_of_edges,
+    read_adjacency_graph,
+    snap_to_adj,
     szudzik64_pair,
     szudzik64_unpair,
 )
 from ._lib import LIB_PATH  # noqa: F401
 
-__all__ = ["WharfMH", "WharfConfig", "generate_batch_of_edges", "szudzik64_pair", "szudzik64_unpair",
-           "DEEPWALK", "NODE2VEC", "RANDOM", "BURNIN", "WEIGHT", "SENTINEL"]
+__all__ = ["WharfMH", "WharfConfig", "generate_batch_of_edges", "read_adjacency_graph", "snap_to_adj",
+           "szudzik64_pair", "szudzik64_unpair", "DEEPWALK", "NODE2VEC", "RANDOM", "BURNIN", "WEIGHT", "SENTINEL"]

@@ -82,6 +82,10 @@ SIGNATURES = {
     "wharf_get_stats": (_I, [_P, _P]),
     "wharf_generate_batch_of_edges": (_I, [_I, _U64, _U64, _U64, _I, _I, C.c_double, C.c_double, C.c_double, _P, _P]),
     "wharf_szudzik64": (_I, [_I, _I, _U64, _P, _P, _P]),
+    "wharf_read_adjacency_graph": (_I, [C.c_char_p, _P, _P, _P, _P]),
+    "wharf_snap_to_adj": (_I, [C.c_char_p, C.c_char_p, _I]),
+    "wharf_write_corpus": (_I, [_P, C.c_char_p, _P, _U64, _I]),
+    "wharf_format_corpus": (_I, [_P, _U64, _U32, C.c_char_p, _I]),
 }
 
 

@@ -739,6 +739,42 @@ int wharf_export_walks_device(wharf_handle* h, uint32_t* dst, int layout)
     return guarded(h, [&] { export_walks_impl(h, dst, layout, hipMemcpyDeviceToDevice); });
 }
 
+int wharf_write_corpus(wharf_handle* h, const char* path, const uint32_t* wids, uint64_t count, int append)
+{
+    return guarded(h, [&] {
+        REQUIRE(h && path, WHARF_E_INVALID, "null argument");
+        h->ensure_walks();
+        const uint64_t total = wids ? count : h->W;
+        const uint64_t chunk = 1 << 20;
+        std::vector<uint64_t> li;
+        std::vector<uint32_t> rows;
+        bool app = append != 0;
+        if (total == 0 && !app) {
+            int rc = wharf_format_corpus(nullptr, 0, h->L, path, 0);
+            REQUIRE(rc == WHARF_OK, WHARF_E_INVALID, std::string("cannot write ") + path);
+        }
+        for (uint64_t c0 = 0; c0 < total; c0 += chunk) {
+            const uint64_t c = std::min(chunk, total - c0);
+            h->sel.ensure(c * h->L * 4);
+            uint64_t* dlist = nullptr;
+            if (wids) {
+                li.resize(c);
+                for (uint64_t i = 0; i < c; i++) li[i] = local_index(h, wids[c0 + i]);
+                h->count.ensure(c * 8);
+                HIPCHK(hipMemcpyAsync(h->count.p, li.data(), c * 8, hipMemcpyHostToDevice, h->s));
+                dlist = h->count.as<uint64_t>();
+            }
+            launch_gather_rows(h->walks.as<uint32_t>(), h->W, h->L, dlist, c0, c, h->sel.as<uint32_t>(), h->s);
+            rows.resize(c * h->L);
+            HIPCHK(hipMemcpyAsync(rows.data(), h->sel.p, c * h->L * 4, hipMemcpyDeviceToHost, h->s));
+            h->sync();
+            int rc = wharf_format_corpus(rows.data(), c, h->L, path, app);
+            REQUIRE(rc == WHARF_OK, WHARF_E_INVALID, std::string("cannot write ") + path);
+            app = true;
+        }
+    });
+}
+
 int wharf_walk_ids(wharf_handle* h, uint32_t* ids)
 {
     return guarded(h, [&] {

@@ -523,6 +523,24 @@ __global__ void k_gather_walk(const uint32_t* __restrict__ walks, uint64_t W, ui
     for (uint32_t p = threadIdx.x; p < L; p += blockDim.x) out[p] = walks[(uint64_t)p * W + li];
 }
 
+// rows out[i][p] = walks[p][li(i)], li(i) = list ? list[i] : base + i
+__global__ void k_gather_rows(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, const uint64_t* __restrict__ list,
+                              uint64_t base, uint64_t count, uint32_t* __restrict__ out)
+{
+    const uint64_t total = count * L;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = t / count, i = t - p * count;   // consecutive threads: consecutive walks of one position
+        const uint64_t li = list ? list[i] : base + i;
+        out[i * L + p] = walks[p * W + li];
+    }
+}
+
+void launch_gather_rows(const uint32_t* walks, uint64_t W, uint32_t L, const uint64_t* list, uint64_t base,
+                        uint64_t count, uint32_t* out, hipStream_t s)
+{
+    if (count) hipLaunchKernelGGL(k_gather_rows, grid_for(count * L, 256), 256, 0, s, walks, W, L, list, base, count, out);
+}
+
 // entries: sort key = (vertex << kb) | (wid*L + pos), value = next
 __global__ void k_index_entries(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc,
                                 uint64_t lo, int kb, const uint64_t* __restrict__ col_base,

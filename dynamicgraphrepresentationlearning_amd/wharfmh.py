@@ -230,6 +230,16 @@ class WharfMH:
         L.check(L.lib.wharf_export_walks_device(self._h, C.c_void_p(device_ptr), 0 if layout == "walk" else 1),
                 self._h, "export_walks_device")
 
+    def write_corpus(self, path: str, walk_ids=None, append: bool = False) -> None:
+        """Text corpus for yskip (vertex-classification.cpp:142-150): one
+        WharfMH::walk line per walk; all owned walks, or `walk_ids` in order."""
+        if walk_ids is None:
+            rc = L.lib.wharf_write_corpus(self._h, path.encode(), None, 0, int(append))
+        else:
+            ids = np.ascontiguousarray(walk_ids, dtype=np.uint32)
+            rc = L.lib.wharf_write_corpus(self._h, path.encode(), _ptr(ids), len(ids), int(append))
+        L.check(rc, self._h, "write_corpus")
+
     def inverted_index(self):
         """Per-vertex ascending (key = wid*L + pos, next) lists (walks/inverted_index.h):
         returns (counts[n], keys, nexts)."""
@@ -254,6 +264,24 @@ def generate_batch_of_edges(edges_number: int, vertices_number: int, batch_seed:
                                                 int(directed), a, b, c, _ptr(out), C.byref(cnt)),
             None, "generate_batch_of_edges")
     return out[: cnt.value].copy()
+
+
+def read_adjacency_graph(path: str):
+    """read_unweighted_graph (common/IO.h:67-106) -> (offsets[n+1] u64, targets[m] u32)."""
+    n, m = C.c_uint64(), C.c_uint64()
+    L.check(L.lib.wharf_read_adjacency_graph(path.encode(), C.byref(n), C.byref(m), None, None), None,
+            "read_adjacency_graph")
+    off = np.zeros(n.value + 1, dtype=np.uint64)
+    adj = np.zeros(max(m.value, 1), dtype=np.uint32)
+    L.check(L.lib.wharf_read_adjacency_graph(path.encode(), C.byref(n), C.byref(m), _ptr(off), _ptr(adj)), None,
+            "read_adjacency_graph")
+    off[n.value] = m.value
+    return off, adj[: m.value]
+
+
+def snap_to_adj(snap_path: str, adj_path: str, symmetric: bool = True) -> None:
+    """experiments/bin/SNAPtoAdj [-s]: SNAP edge list -> AdjacencyGraph text."""
+    L.check(L.lib.wharf_snap_to_adj(snap_path.encode(), adj_path.encode(), int(symmetric)), None, "snap_to_adj")
 
 
 def szudzik64_pair(x, y, device: int = 0) -> np.ndarray:

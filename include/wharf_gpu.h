@@ -168,6 +168,27 @@ int wharf_generate_batch_of_edges(int device, uint64_t edges_number, uint64_t ve
                                   int self_loops, int directed, double a, double b, double c,
                                   uint32_t* out_pairs, uint64_t* count);
 
+/* ---- IO (host side) ------------------------------------------------------ */
+
+/* read_unweighted_graph (libs/compressed_trees/common/IO.h:67-106): Ligra
+ * "AdjacencyGraph" text.  Call with offsets == NULL for n and m, then with
+ * offsets[n] and targets[m]. */
+int wharf_read_adjacency_graph(const char* path, uint64_t* n, uint64_t* m, uint64_t* offsets, uint32_t* targets);
+
+/* The prebuilt experiments/bin/SNAPtoAdj (-s): SNAP edge list ('#' comments)
+ * -> AdjacencyGraph text, symmetrised when `symmetric`, sorted, duplicates and
+ * self loops removed, n = largest id + 1. */
+int wharf_snap_to_adj(const char* snap_path, const char* adj_path, int symmetric);
+
+/* Text corpus for yskip (vertex-classification.cpp:142-150): one line per walk,
+ * WharfMH::walk format "v0 v1 ... " + '\n'.  wids == NULL writes every owned
+ * walk in ascending id order; otherwise the listed (owned) walks in list order
+ * (e.g. the affected ids of an update).  append != 0 appends to the file. */
+int wharf_write_corpus(wharf_handle* h, const char* path, const uint32_t* wids, uint64_t count, int append);
+
+/* Formatting half of wharf_write_corpus for walk-major rows already on the host. */
+int wharf_format_corpus(const uint32_t* rows, uint64_t count, uint32_t walk_length, const char* path, int append);
+
 /* pairings::Szudzik (walks/pairings.h:113-226) on the device, elementwise.
  * op 0: pair(x[i], y[i]) -> z[i]; op 1: unpair(z[i]) -> x[i], y[i].  64-bit
  * unpair uses an exact integer square root (the reference's floor(sqrt(double))
