@@ -44,12 +44,32 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ t, uin
     uint32_t x = mix((uint32_t)li);
     for (int p = 0; p < L; p++) {
         uint64_t slot;
-        if (MODE == 0) slot = __umulhi(x, (uint32_t)n);                          // dep
+        if (MODE == 4) {                                                          // dep + Philox4x32-10 per step
+            uint32_t c0 = (uint32_t)li, c1 = x, c2 = (uint32_t)p, c3 = 0, k0 = 0x5EED, k1 = 0;
+#pragma unroll
+            for (int rr = 0; rr < 10; rr++) {
+                if (rr) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+                const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+                const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+                const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+                c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+            }
+            x = c0;
+        }
+        if (MODE == 0 || MODE == 4) slot = __umulhi(x, (uint32_t)n);             // dep
         else if (MODE == 1) slot = __umulhi(mix((uint32_t)(li * 131 + p)), (uint32_t)n);   // indep
-        else slot = (li + (uint64_t)p * W) % n;                                   // stream
-        const uint4 r = t[slot];
+        else if (MODE == 2) slot = (li + (uint64_t)p * W) % n;                    // stream
+        else slot = __umulhi(x, (uint32_t)n);                                     // dep, nt load
+        uint4 r;
+        if (MODE == 3) {
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(t + slot));
+            r = make_uint4(q.x, q.y, q.z, q.w);
+        } else {
+            r = t[slot];
+        }
         out[(uint64_t)p * W + li] = r.x;
-        x = MODE == 0 ? mix(r.y ^ x) : x + r.y;
+        x = (MODE == 0 || MODE == 3 || MODE == 4) ? mix(r.y ^ x) : x + r.y;
     }
 }
 
@@ -68,13 +88,15 @@ int main(int argc, char** argv)
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
-    const char* names[3] = {"dep", "indep", "stream"};
+    const char* names[5] = {"dep", "indep", "stream", "dep_nt", "dep_philox"};
     for (int rep = 0; rep < 2; rep++)
-        for (int mode = 0; mode < 3; mode++) {
+        for (int mode = 0; mode < 5; mode++) {
             CHK(hipEventRecord(a));
             if (mode == 0) hipLaunchKernelGGL(k_gather<0>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 1) hipLaunchKernelGGL(k_gather<1>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 2) hipLaunchKernelGGL(k_gather<2>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 4) hipLaunchKernelGGL(k_gather<4>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 3) hipLaunchKernelGGL(k_gather<3>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             CHK(hipEventRecord(b));
             CHK(hipEventSynchronize(b));
             float ms;
