@@ -84,8 +84,8 @@ struct wharf_handle {
     uint32_t L = 0, wpv = 0;
     bool anchors = false, has_walks = false;
     uint32_t epoch = 0;
-    DevBuf off, adj, vrec, erec, anchor, row_epoch, off2, adj2, anchor2, ehash;
-    uint64_t ehash_mask = 0;
+    DevBuf off, adj, vrec, erec, anchor, row_epoch, off2, adj2, anchor2, ehash, erec2;
+    uint64_t ehash_mask = 0, ehash_used = 0;   // capacity - 1; occupied slots incl. tombstones
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
     DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, count, pairs, sel;
     wharf_stats st{};
@@ -167,14 +167,18 @@ struct wharf_handle {
         erec.ensure(std::max<uint64_t>(m, 1) * sizeof(ERec));
         launch_vrec(off.as<uint64_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
         launch_erec(adj.as<uint32_t>(), m, vrec.as<ERec>(), erec.as<ERec>(), s);
-        if (anchors) {
-            uint64_t cap = 64;
-            while (cap < 2 * m) cap <<= 1;   // load factor <= 1/2
-            ehash.ensure(cap * 8);
-            ehash_mask = cap - 1;
-            launch_fill_u64(ehash.as<uint64_t>(), cap, kEmptyKey, s);
-            launch_edge_hash_build(off.as<uint64_t>(), n, adj.as<uint32_t>(), ehash.as<uint64_t>(), ehash_mask, s);
-        }
+        if (anchors) build_edge_hash();
+    }
+
+    void build_edge_hash()
+    {
+        uint64_t cap = 64;
+        while (cap < 2 * m) cap <<= 1;   // load factor <= 1/2
+        ehash.ensure(cap * 8);
+        ehash_mask = cap - 1;
+        ehash_used = m;
+        launch_fill_u64(ehash.as<uint64_t>(), cap, kEmptyKey, s);
+        launch_edge_hash_build(off.as<uint64_t>(), n, adj.as<uint32_t>(), ehash.as<uint64_t>(), ehash_mask, s);
     }
 
     WalkArgs walk_args()
@@ -298,7 +302,7 @@ void free_handle(wharf_handle* h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->s) (void)hipStreamSynchronize(h->s);
-    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->ehash, &h->anchor, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
+    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->anchor, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
                       &h->aff, &h->rtab, &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags,
                       &h->chg, &h->cf, &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel})
         b->release();
@@ -407,9 +411,19 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->adj2.ensure(std::max<uint64_t>(m_new, 1) * 4);
         if (h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8);
         launch_new_offsets(h->off.as<uint64_t>(), h->n, bkeys, mb, h->cf.as<uint32_t>(), insert, h->off2.as<uint64_t>(), s);
+        // edge records move with their slot and are patched arithmetically when
+        // a second record buffer fits; otherwise they are rebuilt by a gather
+        bool patch = true;
+        try {
+            h->erec2.ensure(std::max<uint64_t>(m_new, 1) * sizeof(ERec));
+        } catch (const WharfError&) {
+            (void)hipGetLastError();
+            patch = false;
+        }
         launch_move_edges(h->adj.as<uint32_t>(), h->anchors ? h->anchor.as<uint64_t>() : nullptr, h->m,
                           h->runs.as<RunInfo>(), k, bkeys, h->cf.as<uint32_t>(), h->off2.as<uint64_t>(), insert,
-                          h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint64_t>() : nullptr, m_new, s);
+                          h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint64_t>() : nullptr, m_new,
+                          patch ? h->erec.as<ERec>() : nullptr, patch ? h->erec2.as<ERec>() : nullptr, mb, h->epoch, s);
         if (insert)
             launch_place_new(bkeys, mb, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(), h->runstart.as<uint32_t>(), k,
                              h->runs.as<RunInfo>(), h->adj.as<uint32_t>(), h->off2.as<uint64_t>(),
@@ -418,7 +432,26 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         std::swap(h->adj, h->adj2);
         if (h->anchors) std::swap(h->anchor, h->anchor2);
         h->m = m_new;
-        h->build_records();
+        if (patch) {
+            std::swap(h->erec, h->erec2);
+            launch_vrec(h->off.as<uint64_t>(), h->n, h->row_epoch.as<uint32_t>(), h->vrec.as<ERec>(), s);
+            launch_erec_rows(h->runs.as<RunInfo>(), k, h->off.as<uint64_t>(), h->adj.as<uint32_t>(),
+                             h->vrec.as<ERec>(), h->erec.as<ERec>(), s);
+            if (h->anchors) {
+                // the edge set changes by the batch's changing edges only; rebuild when
+                // inserts (and tombstones) push the load past 0.6
+                if (insert && (h->ehash_used + total_chg) * 10 > (h->ehash_mask + 1) * 6) {
+                    h->build_edge_hash();
+                } else {
+                    launch_edge_hash_update(bkeys, mb, h->chg.as<uint32_t>(), insert, h->ehash.as<uint64_t>(),
+                                            h->ehash_mask, s);
+                    if (insert) h->ehash_used += total_chg;
+                }
+            }
+        } else {
+            h->erec2.release();
+            h->build_records();
+        }
         HIPCHK(hipEventRecord(h->ev[1], s));
 
         // 5. rewalk points + suffix re-walk in one pass over the walk matrix

@@ -37,6 +37,7 @@ constexpr uint64_t kOffBits = 40;
 constexpr uint64_t kOffMask = (1ull << kOffBits) - 1;
 constexpr uint64_t kAnchorNone64 = ~0ull;
 constexpr uint64_t kEmptyKey = ~0ull;         // empty slot of the edge hash set
+constexpr uint64_t kTombKey = ~0ull - 1;      // deleted edge (probing continues past it)
 
 __host__ __device__ __forceinline__ ERec make_rec(uint32_t v, uint32_t deg, uint64_t off, uint32_t epoch)
 {

@@ -59,7 +59,10 @@ void launch_new_offsets(const uint64_t* off, uint64_t n, const uint64_t* bkeys, 
                         int insert, uint64_t* noff, hipStream_t s);
 void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunInfo* runs, uint64_t k,
                        const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
-                       uint64_t* nanc, uint64_t cap, hipStream_t s);
+                       uint64_t* nanc, uint64_t cap, const ERec* oerec, ERec* nerec, uint64_t mb, uint32_t epoch,
+                       hipStream_t s);
+void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* nadj, const ERec* vrec,
+                      ERec* erec, hipStream_t s);
 void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf,
                       const uint32_t* run_start, uint64_t k, const RunInfo* runs, const uint32_t* adj,
                       const uint64_t* noff, uint32_t* nadj, uint64_t* nanc, uint64_t cap, hipStream_t s);
@@ -76,6 +79,8 @@ void launch_li_to_wid(const uint64_t* li, uint64_t cnt, uint64_t n, uint64_t n_l
                       hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s);
 void launch_fill_u64(uint64_t* p, uint64_t cnt, uint64_t v, hipStream_t s);
+void launch_edge_hash_update(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, int insert, uint64_t* table,
+                             uint64_t mask, hipStream_t s);
 void launch_edge_hash_build(const uint64_t* off, uint64_t n, const uint32_t* adj, uint64_t* table, uint64_t mask,
                             hipStream_t s);
 void launch_szudzik64(int op, uint64_t cnt, uint64_t* x, uint64_t* y, uint64_t* z, hipStream_t s);

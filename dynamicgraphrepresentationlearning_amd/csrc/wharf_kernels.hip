@@ -288,6 +288,36 @@ __global__ void k_edge_hash_build(const uint64_t* __restrict__ off, uint64_t n, 
     }
 }
 
+// apply a batch to the edge set: insert the new edges / tombstone the deleted ones
+__global__ void k_edge_hash_update(const uint64_t* __restrict__ bkeys, uint64_t mb, const uint32_t* __restrict__ chg,
+                                   int insert, unsigned long long* __restrict__ table, uint64_t mask)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mb; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (!chg[i]) continue;
+        const unsigned long long key = bkeys[i];
+        uint64_t b = (edge_hash(key) & mask) & ~3ull;
+        for (bool done = false; !done; b = (b + 4) & mask) {
+            for (int k = 0; k < 4 && !done; k++) {
+                if (insert) {
+                    const unsigned long long old = atomicCAS(table + b + k, (unsigned long long)kEmptyKey, key);
+                    done = old == kEmptyKey || old == key;
+                } else {
+                    const unsigned long long cur = table[b + k];
+                    if (cur == key) { table[b + k] = kTombKey; done = true; }
+                    else if (cur == kEmptyKey) done = true;   // not present
+                }
+            }
+        }
+    }
+}
+
+void launch_edge_hash_update(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, int insert, uint64_t* table,
+                             uint64_t mask, hipStream_t s)
+{
+    if (mb) hipLaunchKernelGGL(k_edge_hash_update, grid_for(mb, 256), 256, 0, s, bkeys, mb, chg, insert,
+                               (unsigned long long*)table, mask);
+}
+
 void launch_edge_hash_build(const uint64_t* off, uint64_t n, const uint32_t* adj, uint64_t* table, uint64_t mask,
                             hipStream_t s)
 {
@@ -425,10 +455,36 @@ __global__ void k_new_offsets(const uint64_t* __restrict__ off, uint64_t n, cons
 }
 
 // Move every old edge to its slot in the new CSR (one coalesced streaming pass).
+// The record of a target vertex after the batch: its row moved by the number
+// of changing batch edges with a smaller source; a batch source also changed
+// degree and had its samplers reset (epoch).  Pure arithmetic on the run
+// table, so moving the 16-B records needs no gather.
+__device__ __forceinline__ ERec patch_rec(const ERec r, const RunInfo* __restrict__ runs, uint64_t k,
+                                          const uint32_t* __restrict__ cf, uint64_t mb, int insert, uint32_t epoch)
+{
+    const uint32_t v = r.v;
+    uint64_t lo = 0, hi = k;
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (runs[mid].src < v) lo = mid + 1; else hi = mid;
+    }
+    const uint64_t shift = lo < k ? cf[runs[lo].rs] : cf[mb];
+    uint64_t off = r.oe & kOffMask;
+    uint32_t ep = (uint32_t)(r.oe >> kOffBits), deg = r.deg;
+    off = insert ? off + shift : off - shift;
+    if (lo < k && runs[lo].src == v) {
+        const uint32_t d = cf[runs[lo].re] - cf[runs[lo].rs];
+        deg = insert ? deg + d : deg - d;
+        ep = epoch;
+    }
+    return make_rec(v, deg, off, ep);
+}
+
 __global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* __restrict__ anc, uint64_t m,
                              const RunInfo* __restrict__ runs, uint64_t k, const uint64_t* __restrict__ bkeys,
                              const uint32_t* __restrict__ cf, const uint64_t* __restrict__ noff, int insert,
-                             uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc, uint64_t cap)
+                             uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc, uint64_t cap,
+                             const ERec* __restrict__ oerec, ERec* __restrict__ nerec, uint64_t mb, uint32_t epoch)
 {
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
         // last source run whose row starts at or before e
@@ -441,6 +497,7 @@ __global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* _
         if (lo == 0) {
             nadj[e] = x;
             if (nanc) nanc[e] = anc[e];
+            if (nerec) nerec[e] = patch_rec(oerec[e], runs, k, cf, mb, insert, epoch);
             continue;
         }
         const RunInfo ri = runs[lo - 1];
@@ -463,8 +520,24 @@ __global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* _
             if (np >= cap) continue;
             nadj[np] = x;
             if (nanc) nanc[np] = anc[e];
+            if (nerec) nerec[np] = patch_rec(oerec[e], runs, k, cf, mb, insert, epoch);
         }
     }
+}
+
+// records of the rebuilt source rows: erec[slot] = vrec[adj[slot]] (block per run)
+__global__ void k_erec_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ noff,
+                            const uint32_t* __restrict__ nadj, const ERec* __restrict__ vrec, ERec* __restrict__ erec)
+{
+    const uint32_t s = runs[blockIdx.x].src;
+    const uint64_t b = noff[s], e = noff[s + 1];
+    for (uint64_t j = b + threadIdx.x; j < e; j += blockDim.x) erec[j] = vrec[nadj[j]];
+}
+
+void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* nadj, const ERec* vrec,
+                      ERec* erec, hipStream_t s)
+{
+    if (k) hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, noff, nadj, vrec, erec);
 }
 
 // Place the inserted edges (insert only).
@@ -660,8 +733,13 @@ void launch_new_offsets(const uint64_t* off, uint64_t n, const uint64_t* bkeys, 
 { hipLaunchKernelGGL(k_new_offsets, grid_for(n + 1, 256), 256, 0, s, off, n, bkeys, mb, cf, insert, noff); }
 void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunInfo* runs, uint64_t k,
                        const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
-                       uint64_t* nanc, uint64_t cap, hipStream_t s)
-{ if (m) hipLaunchKernelGGL(k_move_edges, grid_for(m, 256), 256, 0, s, adj, anc, m, runs, k, bkeys, cf, noff, insert, nadj, nanc, cap); }
+                       uint64_t* nanc, uint64_t cap, const ERec* oerec, ERec* nerec, uint64_t mb, uint32_t epoch,
+                       hipStream_t s)
+{
+    if (m)
+        hipLaunchKernelGGL(k_move_edges, grid_for(m, 256), 256, 0, s, adj, anc, m, runs, k, bkeys, cf, noff, insert, nadj,
+                           nanc, cap, oerec, nerec, mb, epoch);
+}
 void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf, const uint32_t* run_start,
                       uint64_t k, const RunInfo* runs, const uint32_t* adj, const uint64_t* noff, uint32_t* nadj,
                       uint64_t* nanc, uint64_t cap, hipStream_t s)

@@ -23,6 +23,7 @@ for s in "$@"; do
     bench)  step bench 900 python bench.py ;;
     benchq) step benchq 600 python bench.py --cpu-baseline off ;;
     roof)   step gather_roof 300 tools/gather_roof 3.48 ;;
+    big)    step bigscale 900 python tools/bigscale.py ;;
     det)    step bench_det 900 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     n2v)    step bench_n2v 900 python bench.py --model node2vec --steps 2 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     dist2)  step bench_dist2 900 env WHARF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --scale 20 --samples 29296270 --stream-samples 10000000 --steps 3 --warmup 1 --rewalk-batches 5 ;;
