@@ -216,8 +216,11 @@ def main():
         gs.set_shard(lo, hi) if world == 1 else gs.set_shard(*balanced_shards(
             np.diff(gs.flatten_graph()[0].astype(np.int64)), world)[rank])
         gs.generate_initial_random_walks()
+        gs.generate_initial_random_walks()
+        s1 = gs.stats()
+        gen3 = {"ms": round(s1["last_walk_kernel_ms"], 3), "steps": s1["steps"]}
         out = np.empty(gs.number_of_walks, dtype=np.uint32)
-        lat, aff, gu, wu, kern = [], [], [], [], []
+        lat, aff, gu, wu, kern, rsteps = [], [], [], [], [], []
         for b in range(args.rewalk_batches):
             batch = W.generate_batch_of_edges(5000, n, b, False, False, device=dev)
             barrier()
@@ -230,6 +233,7 @@ def main():
             gu.append(s2["last_graph_update_ms"])
             wu.append(s2["last_walk_update_ms"])
             kern.append(s2["last_walk_kernel_ms"])
+            rsteps.append(s2["steps"])
         lat_all = lat
         if dist:
             tl = torch.tensor(lat, dtype=torch.float64, device=comm_dev)
@@ -244,7 +248,10 @@ def main():
                   "mean_affected_walks_rank0": int(np.mean(aff)),
                   "median_graph_update_ms": round(float(np.median(gu)), 3),
                   "median_walk_update_ms": round(float(np.median(wu)), 3),
-                  "median_rewalk_kernel_ms": round(float(np.median(kern)), 3)}
+                  "median_rewalk_kernel_ms": round(float(np.median(kern)), 3),
+                  "mean_rewalk_steps_rank0": int(np.mean(rsteps)),
+                  "rewalk_Gsteps_per_s": round(float(np.sum(rsteps) / np.sum(kern) / 1e6), 2),
+                  "generation_same_graph": gen3}
         gs.destroy()
 
     if rank == 0:
