@@ -7,6 +7,8 @@
 //                  store/load of one position by a wave is one contiguous 256-B segment
 //   anchor[m]      frozen MH anchor per (cur, slot of prev in adj(cur)) (node2vec MH)
 //   bitmap[n/32]   batch-source set for the rewalk-point scan
+#include <cstdlib>
+
 #include "wharf_kernels.h"
 
 namespace wharf {
@@ -138,110 +140,204 @@ __device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc,
 }
 
 // ---------------------------------------------------------------------------
-// The walk kernel: generation (REWALK=false, wharfmh.h:275-326) and fused
-// rewalk-point scan + suffix re-walk (REWALK=true, wharfmh.h:519-537 + 761-859).
-// One lane per walk; lane li owns walk matrix column li.  The walker carries
-// the record of its current vertex, so a step is ONE dependent 16-B gather:
-// erec[cur.off + pick] = {next vertex, its degree, row offset, row epoch}.
+// The walk kernels.  One lane per walk; lane li owns walk matrix column li.
+// The walker carries the record of its current vertex, so a step is ONE
+// dependent 16-B gather: erec[cur.off + pick] = {next vertex, its degree, row
+// offset, row epoch}.
 // ---------------------------------------------------------------------------
-template <int MODEL, bool DET, bool REWALK>
+
+// One transition cur -> next from position `pos` (deepwalk.h:64-87 /
+// node2vec.h:52-72 through MetropolisHastingsSampler::sample, or the
+// deterministic adj(cur)[Random(wid/n).lrand() % deg] of wharfmh.h:296-304).
+template <int MODEL, bool DET>
+__device__ __forceinline__ Row walk_step(const WalkArgs& a, const Row& rc, const Row& rp, int64_t& ein,
+                                         const uint64_t* __restrict__ rt, uint32_t pos, uint32_t wlo,
+                                         uint32_t whi, uint32_t ep, uint32_t& accepts)
+{
+    if constexpr (DET) {
+        // rt = Random(wid / n) restarted at the walk's first re-walked position
+        return load_rec(a.erec, rc.off + umod64_32(rt[pos], rc.deg));
+    } else {
+        const P4 q = philox4x32_10(wlo, whi, pos, ep | kStreamStep, a.key0, a.key1);
+        const uint32_t ci = (uint32_t)pick32(q.x0, rc.deg);
+        const Row cand = load_rec(a.erec, rc.off + ci);
+        if constexpr (MODEL == kDeepWalk) {
+            accepts++;   // weights are all 1: sample() always accepts
+            return cand;
+        } else {
+            uint32_t acls;
+            const uint32_t ai = anchor_get(a, rc, rp, ein, acls);
+            bool ok = true;   // proposing the anchor itself is always accepted
+            if (ai != ci) {
+                const float wc = weight<MODEL>(a, rp, cand.v);
+                const float wa = class_weight(a, acls);
+                ok = (wa < wc) || (u01(q.x1, q.x2) <= (double)wc / (double)wa);
+            }
+            accepts += ok;
+            ein = (int64_t)(rc.off + (ok ? ci : ai));
+            return ok ? cand : load_rec(a.erec, rc.off + ai);
+        }
+    }
+}
+
+// Walker state at position p of walk wid (cur = its vertex): the rows of cur
+// and prev and, for node2vec MH, the slot of the edge prev -> cur.
+template <int MODEL, bool DET>
+__device__ __forceinline__ void walk_state(const WalkArgs& a, uint32_t cur, uint32_t prev, uint32_t p, uint32_t wlo,
+                                           uint32_t whi, uint32_t ep, Row& rc, Row& rp, int64_t& ein)
+{
+    rc = load_rec(a.vrec, cur);
+    rp = rc;
+    ein = -1;
+    if constexpr (MODEL == kNode2Vec && !DET) {
+        if (p > 0) {
+            rp = load_rec(a.vrec, prev);
+        } else if (rc.deg) {
+            // Node2Vec::initial_state: prev = random neighbour (node2vec.h:42-50)
+            const P4 q = philox4x32_10(wlo, whi, 0, ep | kStreamPrev, a.key0, a.key1);
+            rp = load_rec(a.erec, rc.off + pick32(q.x0, rc.deg));
+        }
+        if (rc.deg) ein = row_find(a.adj, rp, rc.v);
+    }
+}
+
+// Generation (wharfmh.h:275-326): every lane of a wave writes the same
+// position at the same time -> one contiguous 256-B store per step.
+template <int MODEL, bool DET>
 __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
 {
-    const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t steps = 0, accepts = 0;
-    if (li < a.W) {
-        const ERec* __restrict__ vrec = a.vrec;
-        const ERec* __restrict__ erec = a.erec;
-        uint32_t* __restrict__ walks = a.walks;
-        const uint64_t W = a.W;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t* __restrict__ walks = a.walks;
+    const uint64_t W = a.W;
+    for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += stride) {
         const uint64_t r = li / a.n_loc;
         const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
         const uint64_t wid = r * a.n + v;
-
-        uint32_t p = 0, cur = v;
-        bool go = true;
-        if constexpr (REWALK) {
-            // min position of any batch source in this walk, over the old corpus
-            p = kNoRewalk;
-            for (uint32_t pos = 0; pos < a.L; pos++) {
-                const uint32_t x = walks[(uint64_t)pos * W + li];
-                if (x == kSent) break;
-                if ((a.bitmap[x >> 5] >> (x & 31)) & 1u) { p = pos; cur = x; break; }
-            }
-            a.aff[li] = (uint8_t)p;
-            go = p != kNoRewalk && !a.scan_only;
-        } else {
-            walks[li] = v;
+        const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
+        const uint64_t* __restrict__ rt = DET ? a.rtab + r * a.L : nullptr;
+        walks[li] = v;
+        Row rc, rp;
+        int64_t ein;
+        walk_state<MODEL, DET>(a, v, v, 0, wlo, whi, ep, rc, rp, ein);
+        uint32_t pos = 0;
+        for (; pos + 1 < a.L; pos++) {
+            if (rc.deg == 0) break;   // dead end: the walk stops (reference: lrand() % 0)
+            const Row nx = walk_step<MODEL, DET>(a, rc, rp, ein, rt, pos, wlo, whi, ep, accepts);
+            walks[(uint64_t)(pos + 1) * W + li] = nx.v;
+            steps++;
+            rp = rc;
+            rc = nx;
         }
-        if (go) {
-            const uint32_t ep = a.epoch << 4;
-            const uint32_t wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
-            Row rc = load_rec(vrec, cur);
-            Row rp = rc;
-            int64_t ein = -1;   // slot of the edge prev -> cur (node2vec anchor cache key)
-            if constexpr (MODEL == kNode2Vec && !DET) {
-                if (p > 0) {
-                    rp = load_rec(vrec, walks[(uint64_t)(p - 1) * W + li]);
-                } else if (rc.deg) {
-                    // Node2Vec::initial_state: prev = random neighbour (node2vec.h:42-50)
-                    const P4 q = philox4x32_10(wlo, whi, 0, ep | kStreamPrev, a.key0, a.key1);
-                    rp = load_rec(erec, rc.off + pick32(q.x0, rc.deg));
-                }
-                if (rc.deg) ein = row_find(a.adj, rp, rc.v);
-            }
-            const uint64_t* __restrict__ rt = DET ? a.rtab + r * a.L : nullptr;
-            uint32_t pos = p;
-            for (; pos + 1 < a.L; pos++) {
-                if (rc.deg == 0) break;   // dead end: the walk stops (reference: lrand() % 0)
-                Row nx;
-                if constexpr (DET) {
-                    // Random(wid / n) restarted at the walk's first re-walked position
-                    nx = load_rec(erec, rc.off + umod64_32(rt[pos - p], rc.deg));
-                } else {
-                    const P4 q = philox4x32_10(wlo, whi, pos, ep | kStreamStep, a.key0, a.key1);
-                    const uint32_t ci = (uint32_t)pick32(q.x0, rc.deg);
-                    const Row cand = load_rec(erec, rc.off + ci);
-                    if constexpr (MODEL == kDeepWalk) {
-                        nx = cand;   // weights are all 1: sample() always accepts
-                        accepts++;
-                    } else {
-                        uint32_t acls;
-                        const uint32_t ai = anchor_get(a, rc, rp, ein, acls);
-                        bool ok = true;   // proposing the anchor itself is always accepted
-                        if (ai != ci) {
-                            const float wc = weight<MODEL>(a, rp, cand.v);
-                            const float wa = class_weight(a, acls);
-                            ok = (wa < wc) || (u01(q.x1, q.x2) <= (double)wc / (double)wa);
-                        }
-                        nx = ok ? cand : load_rec(erec, rc.off + ai);
-                        accepts += ok;
-                        ein = (int64_t)(rc.off + (ok ? ci : ai));
-                    }
-                }
-                walks[(uint64_t)(pos + 1) * W + li] = nx.v;
-                steps++;
-                rp = rc;
-                rc = nx;
-            }
-            for (pos = pos + 1; pos < a.L; pos++) walks[(uint64_t)pos * W + li] = kSent;
-        }
+        for (pos = pos + 1; pos < a.L; pos++) walks[(uint64_t)pos * W + li] = kSent;
     }
     wave_add(a.counters + 0, steps);
     wave_add(a.counters + 1, accepts);
 }
 
+// Fused rewalk-point scan + suffix re-walk (wharfmh.h:519-537 + 761-859).
+// The rewalk point of a walk is the first position holding a batch source;
+// positions after it are re-sampled on the updated graph.  Rewalk points
+// differ from lane to lane, so a lane-at-its-own-pace loop would make every
+// store of a wave hit 64 different rows (4-B partial-line writes, measured
+// 1.4x slower).  Instead each wave sweeps positions in lock step: at
+// position pos a lane is still scanning (reads the old value, checks the
+// bitmap), walking (writes a new vertex) or done; whenever any lane of the
+// wave writes, all lanes write (scanning lanes their old value), so each row
+// of a wave is one full 256-B store.
+enum : uint32_t { kLaneScan = 0, kLaneWalk = 1, kLaneDone = 2 };
+
+template <int MODEL, bool DET>
+__global__ __launch_bounds__(256) void k_rewalk(WalkArgs a)
+{
+    uint32_t steps = 0, accepts = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t* __restrict__ walks = a.walks;
+    const uint64_t W = a.W;
+    const uint32_t L = a.L;
+    for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += stride) {
+        const uint64_t r = li / a.n_loc;
+        const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
+        const uint64_t wid = r * a.n + v;
+        const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
+        const uint64_t* __restrict__ rt = DET ? a.rtab + r * L : nullptr;
+        uint32_t mode = kLaneScan, p = kNoRewalk;
+        uint32_t x = v, xprev = v;                       // old value at pos, at pos - 1
+        uint32_t xn = L > 1 ? walks[W + li] : kSent;     // old value at pos + 1 (prefetched)
+        Row rc, rp;
+        rc.deg = 0;
+        int64_t ein = -1;
+        for (uint32_t pos = 0; pos < L; pos++) {
+            uint32_t val = kSent;
+            bool fresh = false;
+            if (mode == kLaneWalk) {
+                if (rc.deg) {
+                    const Row nx = walk_step<MODEL, DET>(a, rc, rp, ein, rt, DET ? pos - 1 - p : pos - 1, wlo, whi,
+                                                         ep, accepts);
+                    val = nx.v;
+                    steps++;
+                    rp = rc;
+                    rc = nx;
+                }
+                fresh = true;
+            } else if (mode == kLaneScan) {
+                if (pos > 0) {
+                    xprev = x;
+                    x = xn;
+                    if (pos + 1 < L && x != kSent) xn = walks[(uint64_t)(pos + 1) * W + li];
+                }
+                val = x;
+                if (x == kSent) {
+                    mode = kLaneDone;   // old walk ended: no batch source on it
+                } else if ((a.bitmap[x >> 5] >> (x & 31)) & 1u) {
+                    p = pos;
+                    mode = a.scan_only ? kLaneDone : kLaneWalk;
+                    if (!a.scan_only) walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, rc, rp, ein);
+                }
+            }
+            if (!a.scan_only && __any(fresh)) {
+                // kLaneDone lanes: unaffected (their old walk is kSent from
+                // here on) — the same value is rewritten
+                walks[(uint64_t)pos * W + li] = val;
+            }
+            if (!__any(mode != kLaneDone)) break;
+        }
+        a.aff[li] = (uint8_t)p;
+    }
+    wave_add(a.counters + 0, steps);
+    wave_add(a.counters + 1, accepts);
+}
+
+// Blocks for the walk kernels: one walk per lane by default; a smaller grid of
+// lanes each looping over several walks with WHARF_WALK_BLOCKS_PER_CU=k
+// (k blocks of 256 per CU; 0 = one walk per lane).
+static unsigned walk_grid(uint64_t W)
+{
+    static int cus = -1, per_cu = 0;
+    if (cus < 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        const char* e = getenv("WHARF_WALK_BLOCKS_PER_CU");
+        per_cu = e ? atoi(e) : 0;
+    }
+    const uint64_t full = (W + 255) / 256;
+    if (per_cu <= 0) return (unsigned)full;
+    return (unsigned)std::min<uint64_t>(full, (uint64_t)cus * per_cu);
+}
+
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
 {
     if (a.W == 0) return;
-    const dim3 grid((unsigned)((a.W + 255) / 256)), block(256);
-#define WHARF_LAUNCH(M, D, R) hipLaunchKernelGGL((k_walk<M, D, R>), grid, block, 0, s, a)
-    if (a.det) {
-        if (rewalk) WHARF_LAUNCH(kDeepWalk, true, true); else WHARF_LAUNCH(kDeepWalk, true, false);
-    } else if (a.model == kDeepWalk) {
-        if (rewalk) WHARF_LAUNCH(kDeepWalk, false, true); else WHARF_LAUNCH(kDeepWalk, false, false);
-    } else {
-        if (rewalk) WHARF_LAUNCH(kNode2Vec, false, true); else WHARF_LAUNCH(kNode2Vec, false, false);
-    }
+    const dim3 grid(walk_grid(a.W)), block(256);
+#define WHARF_LAUNCH(M, D)                                                        \
+    do {                                                                          \
+        if (rewalk) hipLaunchKernelGGL((k_rewalk<M, D>), grid, block, 0, s, a);   \
+        else hipLaunchKernelGGL((k_walk<M, D>), grid, block, 0, s, a);            \
+    } while (0)
+    if (a.det) WHARF_LAUNCH(kDeepWalk, true);
+    else if (a.model == kDeepWalk) WHARF_LAUNCH(kDeepWalk, false);
+    else WHARF_LAUNCH(kNode2Vec, false);
 #undef WHARF_LAUNCH
 }
 

@@ -22,6 +22,9 @@ for s in "$@"; do
     bench18) step bench_s18 600 python bench.py --scale 18 --samples 7324270 --steps 3 --warmup 1 --cpu-baseline off ;;
     bench)  step bench 900 python bench.py ;;
     benchq) step benchq 600 python bench.py --cpu-baseline off ;;
+    rwsweep) for b in 0 8 16 32 64; do
+               step rw_bpc$b 600 env WHARF_WALK_BLOCKS_PER_CU=$b python bench.py --steps 2 --warmup 1 --rewalk-batches 10 --cpu-baseline off
+             done ;;
     roof)   step gather_roof 300 tools/gather_roof 3.48 ;;
     big)    step bigscale 900 python tools/bigscale.py ;;
     det)    step bench_det 900 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Where does a configs[2] re-walk spend its time?  Times, per 10k-edge insert
+batch, the rewalk-point scan alone (apply_walk_updates=False: the scan still
+runs and reports the affected walks) and the fused scan + re-walk.
+
+    python tools/rewalk_probe.py [--batches 6]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=22)
+    ap.add_argument("--samples", type=int, default=43_000_000)
+    ap.add_argument("--batches", type=int, default=6)
+    ap.add_argument("--model", default="deepwalk")
+    a = ap.parse_args()
+    import dynamicgraphrepresentationlearning_amd as W
+    n = 1 << a.scale
+    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, deterministic=False, seed=5,
+                        model=W.NODE2VEC if a.model == "node2vec" else W.DEEPWALK)
+    g = W.WharfMH.from_rmat(n, a.samples, 2 * n, seed=2, config=cfg)
+    g.generate_initial_random_walks()
+    res = {"scan_only_ms": [], "fused_ms": [], "affected": [], "steps": []}
+    for b in range(a.batches):
+        batch = W.generate_batch_of_edges(5000, n, 100 + b, False, False)
+        aff = g.insert_edges_batch(batch, apply_walk_updates=False)
+        res["scan_only_ms"].append(g.stats()["last_walk_update_ms"])
+        batch2 = W.generate_batch_of_edges(5000, n, 500 + b, False, False)
+        aff2 = g.insert_edges_batch(batch2, apply_walk_updates=True)
+        st = g.stats()
+        res["fused_ms"].append(st["last_walk_update_ms"])
+        res["affected"].append(len(aff2))
+        res["steps"].append(st["steps"])
+        print(f"batch {b}: scan-only {res['scan_only_ms'][-1]:.2f} ms ({len(aff)} affected), "
+              f"fused {st['last_walk_update_ms']:.2f} ms ({len(aff2)} affected, {st['steps']} steps)", flush=True)
+    print(json.dumps({k: float(np.median(v)) for k, v in res.items()}))
+    g.destroy()
+
+
+if __name__ == "__main__":
+    main()
