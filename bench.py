@@ -219,7 +219,9 @@ def main():
         gs.generate_initial_random_walks()
         s1 = gs.stats()
         gen3 = {"ms": round(s1["last_walk_kernel_ms"], 3), "steps": s1["steps"]}
-        out = np.empty(gs.number_of_walks, dtype=np.uint32)
+        # affected walk ids stay in HBM (WHARF_AFFECTED_DEVICE); the host-list
+        # variant (PCIe-inclusive, the reference's return value) is timed after
+        out = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
         lat, aff, gu, wu, kern, rsteps = [], [], [], [], [], []
         for b in range(args.rewalk_batches):
             batch = W.generate_batch_of_edges(5000, n, b, False, False, device=dev)
@@ -234,6 +236,15 @@ def main():
             wu.append(s2["last_walk_update_ms"])
             kern.append(s2["last_walk_kernel_ms"])
             rsteps.append(s2["steps"])
+        hout = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, pin_memory=True).numpy().view(np.uint32)
+        lat_host = []
+        for b in range(args.rewalk_batches, args.rewalk_batches + min(5, args.rewalk_batches)):
+            batch = W.generate_batch_of_edges(5000, n, b, False, False, device=dev)
+            barrier()
+            t1 = time.perf_counter()
+            gs.insert_edges_batch(batch, remove_dups=True, out=hout)
+            barrier()
+            lat_host.append((time.perf_counter() - t1) * 1e3)
         lat_all = lat
         if dist:
             tl = torch.tensor(lat, dtype=torch.float64, device=comm_dev)
@@ -245,6 +256,7 @@ def main():
                               f"undirected), re-walk applied",
                   "batches": args.rewalk_batches, "edges_per_batch": int(len(batch)),
                   "median_ms": round(float(np.median(lat_all)), 3), "p90_ms": round(float(np.percentile(lat_all, 90)), 3),
+                  "median_ms_ids_to_host_pinned": round(float(np.median(lat_host)), 3),
                   "mean_affected_walks_rank0": int(np.mean(aff)),
                   "median_graph_update_ms": round(float(np.median(gu)), 3),
                   "median_walk_update_ms": round(float(np.median(wu)), 3),

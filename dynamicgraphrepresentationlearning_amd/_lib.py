@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libwharf_gpu.so")
 WHARF_OK = 0
 WHARF_DEEPWALK, WHARF_NODE2VEC = 0, 1
 WHARF_INIT_RANDOM, WHARF_INIT_BURNIN, WHARF_INIT_WEIGHT = 0, 1, 2
-WHARF_SORTED, WHARF_REMOVE_DUPS, WHARF_APPLY_WALK_UPDATES = 1, 2, 4
+WHARF_SORTED, WHARF_REMOVE_DUPS, WHARF_APPLY_WALK_UPDATES, WHARF_AFFECTED_DEVICE = 1, 2, 4, 8
 SENTINEL = 0xFFFFFFFE
 
 

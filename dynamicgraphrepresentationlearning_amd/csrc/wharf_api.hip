@@ -87,7 +87,7 @@ struct wharf_handle {
     DevBuf off, adj, vrec, erec, anchor, row_epoch, off2, adj2, anchor2, ehash, erec2;
     uint64_t ehash_mask = 0, ehash_used = 0;   // capacity - 1; occupied slots incl. tombstones
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
-    DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, count, pairs, sel;
+    DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, rtabs, count, pairs, sel;
     wharf_stats st{};
     std::string err;
 
@@ -410,7 +410,10 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->off2.ensure((h->n + 1) * 8);
         h->adj2.ensure(std::max<uint64_t>(m_new, 1) * 4);
         if (h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8);
-        launch_new_offsets(h->off.as<uint64_t>(), h->n, bkeys, mb, h->cf.as<uint32_t>(), insert, h->off2.as<uint64_t>(), s);
+        RunIndex rx;
+        h->rtabs.ensure(run_tables_words(h->n, h->m) * 4);
+        launch_run_tables(h->runs.as<RunInfo>(), k, h->n, h->m, h->rtabs.as<uint32_t>(), &rx, s);
+        launch_new_offsets(h->off.as<uint64_t>(), h->n, rx, h->cf.as<uint32_t>(), mb, insert, h->off2.as<uint64_t>(), s);
         // edge records move with their slot and are patched arithmetically when
         // a second record buffer fits; otherwise they are rebuilt by a gather
         bool patch = true;
@@ -421,7 +424,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             patch = false;
         }
         launch_move_edges(h->adj.as<uint32_t>(), h->anchors ? h->anchor.as<uint64_t>() : nullptr, h->m,
-                          h->runs.as<RunInfo>(), k, bkeys, h->cf.as<uint32_t>(), h->off2.as<uint64_t>(), insert,
+                          rx, bkeys, h->cf.as<uint32_t>(), h->off2.as<uint64_t>(), insert,
                           h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint64_t>() : nullptr, m_new,
                           patch ? h->erec.as<ERec>() : nullptr, patch ? h->erec2.as<ERec>() : nullptr, mb, h->epoch, s);
         if (insert)
@@ -474,9 +477,13 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             uint64_t naff = 0;
             HIPCHK(hipMemcpyAsync(&naff, c, 8, hipMemcpyDeviceToHost, s));
             h->sync();
-            launch_li_to_wid(out, naff, h->n, h->n_loc, h->lo, h->pairs.as<uint32_t>(), s);
-            if (affected_out && naff)
-                HIPCHK(hipMemcpyAsync(affected_out, h->pairs.p, naff * 4, hipMemcpyDeviceToHost, s));
+            if (affected_out && (flags & WHARF_AFFECTED_DEVICE)) {
+                launch_li_to_wid(out, naff, h->n, h->n_loc, h->lo, affected_out, s);
+            } else {
+                launch_li_to_wid(out, naff, h->n, h->n_loc, h->lo, h->pairs.as<uint32_t>(), s);
+                if (affected_out && naff)
+                    HIPCHK(hipMemcpyAsync(affected_out, h->pairs.p, naff * 4, hipMemcpyDeviceToHost, s));
+            }
             h->sync();
             h->st.affected = naff;
             if (n_affected) *n_affected = naff;

@@ -39,6 +39,26 @@ struct RunInfo {
     uint32_t src, rs, re, pad;
 };
 
+// bucketed lookup tables over the source-run table (k_run_tables)
+struct RunIndex {
+    const RunInfo* runs;
+    uint64_t k;
+    const uint32_t* vtab;   // [(n >> vs) + 2]
+    const uint32_t* etab;   // [(m >> es) + 2]
+    uint32_t vs, es;
+};
+// bucket shift so a table over [0, x] has at most ~2^target entries
+inline uint32_t run_table_shift(uint64_t x, uint32_t target)
+{
+    uint32_t b = 0;
+    while (b < 63 && (x >> b) >= (1ull << target)) b++;
+    return b;
+}
+inline uint64_t run_tables_words(uint64_t n, uint64_t m)
+{
+    return (n >> run_table_shift(n, 18)) + 2 + (m >> run_table_shift(m, 20)) + 2;
+}
+
 unsigned grid_for(uint64_t work, unsigned block);
 
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s);
@@ -55,9 +75,11 @@ void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off
 void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_t s);
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
                      RunInfo* runs, uint32_t* bitmap, uint32_t* row_epoch, uint32_t epoch, hipStream_t s);
-void launch_new_offsets(const uint64_t* off, uint64_t n, const uint64_t* bkeys, uint64_t mb, const uint32_t* cf,
-                        int insert, uint64_t* noff, hipStream_t s);
-void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunInfo* runs, uint64_t k,
+void launch_run_tables(const RunInfo* runs, uint64_t k, uint64_t n, uint64_t m, uint32_t* tabs, RunIndex* x,
+                       hipStream_t s);
+void launch_new_offsets(const uint64_t* off, uint64_t n, const RunIndex& x, const uint32_t* cf, uint64_t mb, int insert,
+                        uint64_t* noff, hipStream_t s);
+void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunIndex& x,
                        const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
                        uint64_t* nanc, uint64_t cap, const ERec* oerec, ERec* nerec, uint64_t mb, uint32_t epoch,
                        hipStream_t s);

@@ -534,18 +534,67 @@ __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* _
     }
 }
 
+// Bucketed index over the source-run table: vtab[b] = first run with
+// src >= b << vs, etab[b] = first run with row offset >= b << es.  A lookup
+// reads one table pair (L2-resident) and binary-searches the few runs of one
+// bucket instead of log2(k) dependent probes over the whole table per edge.
+__global__ void k_run_tables(const RunInfo* __restrict__ runs, uint64_t k, uint32_t* __restrict__ vtab, uint64_t nbv,
+                             uint32_t vs, uint32_t* __restrict__ etab, uint64_t nbe, uint32_t es)
+{
+    const uint64_t nb = nbv > nbe ? nbv : nbe;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
+        if (b < nbv) {
+            const uint64_t t = b << vs;
+            uint64_t lo = 0, hi = k;
+            while (lo < hi) {
+                const uint64_t mid = lo + ((hi - lo) >> 1);
+                if (runs[mid].src < t) lo = mid + 1; else hi = mid;
+            }
+            vtab[b] = (uint32_t)lo;
+        }
+        if (b < nbe) {
+            const uint64_t t = b << es;
+            uint64_t lo = 0, hi = k;
+            while (lo < hi) {
+                const uint64_t mid = lo + ((hi - lo) >> 1);
+                if (runs[mid].off < t) lo = mid + 1; else hi = mid;
+            }
+            etab[b] = (uint32_t)lo;
+        }
+    }
+}
+
+// first run with src >= v
+__device__ __forceinline__ uint64_t run_lower_src(const RunIndex& x, uint32_t v)
+{
+    const uint64_t b = (uint64_t)v >> x.vs;
+    uint64_t lo = x.vtab[b], hi = x.vtab[b + 1];
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (x.runs[mid].src < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// first run whose row starts after slot e
+__device__ __forceinline__ uint64_t run_upper_off(const RunIndex& x, uint64_t e)
+{
+    const uint64_t b = e >> x.es;
+    uint64_t lo = x.etab[b], hi = x.etab[b + 1];
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (x.runs[mid].off <= e) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
 // new_off[v] = off[v] +/- (changing batch edges with src < v)
-__global__ void k_new_offsets(const uint64_t* __restrict__ off, uint64_t n, const uint64_t* __restrict__ bkeys,
-                              uint64_t mb, const uint32_t* __restrict__ cf, int insert, uint64_t* __restrict__ noff)
+__global__ void k_new_offsets(const uint64_t* __restrict__ off, uint64_t n, RunIndex x, const uint32_t* __restrict__ cf,
+                              uint64_t mb, int insert, uint64_t* __restrict__ noff)
 {
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t t = v << 32;
-        uint64_t lo = 0, hi = mb;
-        while (lo < hi) {
-            const uint64_t mid = lo + ((hi - lo) >> 1);
-            if (bkeys[mid] < t) lo = mid + 1; else hi = mid;
-        }
-        const uint64_t c = cf[lo];
+        const uint64_t j = v < n ? run_lower_src(x, (uint32_t)v) : x.k;
+        const uint64_t c = cf[j < x.k ? x.runs[j].rs : mb];
         noff[v] = insert ? off[v] + c : off[v] - c;
     }
 }
@@ -555,15 +604,13 @@ __global__ void k_new_offsets(const uint64_t* __restrict__ off, uint64_t n, cons
 // of changing batch edges with a smaller source; a batch source also changed
 // degree and had its samplers reset (epoch).  Pure arithmetic on the run
 // table, so moving the 16-B records needs no gather.
-__device__ __forceinline__ ERec patch_rec(const ERec r, const RunInfo* __restrict__ runs, uint64_t k,
-                                          const uint32_t* __restrict__ cf, uint64_t mb, int insert, uint32_t epoch)
+__device__ __forceinline__ ERec patch_rec(const ERec r, const RunIndex& x, const uint32_t* __restrict__ cf, uint64_t mb,
+                                          int insert, uint32_t epoch)
 {
+    const RunInfo* __restrict__ runs = x.runs;
+    const uint64_t k = x.k;
     const uint32_t v = r.v;
-    uint64_t lo = 0, hi = k;
-    while (lo < hi) {
-        const uint64_t mid = lo + ((hi - lo) >> 1);
-        if (runs[mid].src < v) lo = mid + 1; else hi = mid;
-    }
+    const uint64_t lo = run_lower_src(x, v);
     const uint64_t shift = lo < k ? cf[runs[lo].rs] : cf[mb];
     uint64_t off = r.oe & kOffMask;
     uint32_t ep = (uint32_t)(r.oe >> kOffBits), deg = r.deg;
@@ -577,23 +624,20 @@ __device__ __forceinline__ ERec patch_rec(const ERec r, const RunInfo* __restric
 }
 
 __global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* __restrict__ anc, uint64_t m,
-                             const RunInfo* __restrict__ runs, uint64_t k, const uint64_t* __restrict__ bkeys,
+                             RunIndex rx, const uint64_t* __restrict__ bkeys,
                              const uint32_t* __restrict__ cf, const uint64_t* __restrict__ noff, int insert,
                              uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc, uint64_t cap,
                              const ERec* __restrict__ oerec, ERec* __restrict__ nerec, uint64_t mb, uint32_t epoch)
 {
+    const RunInfo* __restrict__ runs = rx.runs;
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
         // last source run whose row starts at or before e
-        uint64_t lo = 0, hi = k;
-        while (lo < hi) {
-            const uint64_t mid = lo + ((hi - lo) >> 1);
-            if (runs[mid].off <= e) lo = mid + 1; else hi = mid;
-        }
+        const uint64_t lo = run_upper_off(rx, e);
         const uint32_t x = adj[e];
         if (lo == 0) {
             nadj[e] = x;
             if (nanc) nanc[e] = anc[e];
-            if (nerec) nerec[e] = patch_rec(oerec[e], runs, k, cf, mb, insert, epoch);
+            if (nerec) nerec[e] = patch_rec(oerec[e], rx, cf, mb, insert, epoch);
             continue;
         }
         const RunInfo ri = runs[lo - 1];
@@ -616,7 +660,7 @@ __global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* _
             if (np >= cap) continue;
             nadj[np] = x;
             if (nanc) nanc[np] = anc[e];
-            if (nerec) nerec[np] = patch_rec(oerec[e], runs, k, cf, mb, insert, epoch);
+            if (nerec) nerec[np] = patch_rec(oerec[e], rx, cf, mb, insert, epoch);
         }
     }
 }
@@ -824,16 +868,29 @@ void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
                      RunInfo* runs, uint32_t* bitmap, uint32_t* row_epoch, uint32_t epoch, hipStream_t s)
 { hipLaunchKernelGGL(k_run_info, grid_for(k, 256), 256, 0, s, bkeys, run_start, k, mb, off, runs, bitmap, row_epoch, epoch); }
-void launch_new_offsets(const uint64_t* off, uint64_t n, const uint64_t* bkeys, uint64_t mb, const uint32_t* cf, int insert,
+void launch_run_tables(const RunInfo* runs, uint64_t k, uint64_t n, uint64_t m, uint32_t* tabs, RunIndex* x,
+                       hipStream_t s)
+{
+    x->runs = runs;
+    x->k = k;
+    x->vs = run_table_shift(n, 18);
+    x->es = run_table_shift(m, 20);
+    const uint64_t nbv = (n >> x->vs) + 2, nbe = (m >> x->es) + 2;
+    x->vtab = tabs;
+    x->etab = tabs + nbv;
+    hipLaunchKernelGGL(k_run_tables, grid_for(std::max(nbv, nbe), 256), 256, 0, s, runs, k, tabs, nbv, x->vs,
+                       tabs + nbv, nbe, x->es);
+}
+void launch_new_offsets(const uint64_t* off, uint64_t n, const RunIndex& x, const uint32_t* cf, uint64_t mb, int insert,
                         uint64_t* noff, hipStream_t s)
-{ hipLaunchKernelGGL(k_new_offsets, grid_for(n + 1, 256), 256, 0, s, off, n, bkeys, mb, cf, insert, noff); }
-void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunInfo* runs, uint64_t k,
+{ hipLaunchKernelGGL(k_new_offsets, grid_for(n + 1, 256), 256, 0, s, off, n, x, cf, mb, insert, noff); }
+void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunIndex& x,
                        const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
                        uint64_t* nanc, uint64_t cap, const ERec* oerec, ERec* nerec, uint64_t mb, uint32_t epoch,
                        hipStream_t s)
 {
     if (m)
-        hipLaunchKernelGGL(k_move_edges, grid_for(m, 256), 256, 0, s, adj, anc, m, runs, k, bkeys, cf, noff, insert, nadj,
+        hipLaunchKernelGGL(k_move_edges, grid_for(m, 256), 256, 0, s, adj, anc, m, x, bkeys, cf, noff, insert, nadj,
                            nanc, cap, oerec, nerec, mb, epoch);
 }
 void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf, const uint32_t* run_start,

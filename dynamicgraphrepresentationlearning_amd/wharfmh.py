@@ -171,6 +171,15 @@ class WharfMH:
         flags = (L.WHARF_SORTED if sorted else 0) | (L.WHARF_REMOVE_DUPS if remove_dups else 0) | \
                 (L.WHARF_APPLY_WALK_UPDATES if apply_walk_updates else 0)
         W = max(self.number_of_walks, 1)
+        if out is not None and getattr(out, "is_cuda", False):
+            # device output (torch int32/uint32 tensor on this handle's GPU): ids stay in HBM
+            import torch
+            if out.dtype not in (torch.int32, torch.uint32) or out.numel() < W or not out.is_contiguous():
+                raise ValueError("device out must be a contiguous 32-bit tensor with >= number_of_walks entries")
+            cnt = C.c_uint64()
+            L.check(fn(self._h, len(e), _ptr(e), flags | L.WHARF_AFFECTED_DEVICE, C.c_void_p(out.data_ptr()),
+                       C.byref(cnt)), self._h, fn.__name__)
+            return out[: cnt.value]
         buf = out if out is not None else np.empty(W, dtype=np.uint32)
         if buf.dtype != np.uint32 or len(buf) < W or not buf.flags.c_contiguous:
             raise ValueError("out must be a contiguous uint32 array with >= number_of_walks entries")
@@ -181,7 +190,8 @@ class WharfMH:
     def insert_edges_batch(self, edges, sorted: bool = False, remove_dups: bool = False, nn: int | None = None,
                            apply_walk_updates: bool = True, run_seq: bool = False, out=None) -> np.ndarray:
         """wharfmh.h:439.  `edges`: (m, 2) (src, dst).  Returns the affected walk ids
-        (ascending; a view of `out` when given).  `nn` and `run_seq` are CPU
+        (ascending; a view of `out` when given — a torch tensor on the GPU keeps
+        them in HBM, WHARF_AFFECTED_DEVICE).  `nn` and `run_seq` are CPU
         sort/scheduling hints of the reference and have no effect here; the
         caller's buffer is not modified."""
         return self._update(L.lib.wharf_insert_edges, edges, sorted, remove_dups, apply_walk_updates, out)

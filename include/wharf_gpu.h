@@ -46,7 +46,8 @@ enum { WHARF_DEEPWALK = 0, WHARF_NODE2VEC = 1 };
 /* types::SamplerInitStartegy (config/types.h:31) */
 enum { WHARF_INIT_RANDOM = 0, WHARF_INIT_BURNIN = 1, WHARF_INIT_WEIGHT = 2 };
 /* insert_edges_batch / delete_edges_batch boolean arguments (wharfmh.h:439,588) */
-enum { WHARF_SORTED = 1, WHARF_REMOVE_DUPS = 2, WHARF_APPLY_WALK_UPDATES = 4 };
+enum { WHARF_SORTED = 1, WHARF_REMOVE_DUPS = 2, WHARF_APPLY_WALK_UPDATES = 4,
+       WHARF_AFFECTED_DEVICE = 8 /* affected_out is device memory of the handle's GPU (no PCIe copy) */ };
 
 #define WHARF_SENTINEL 0xFFFFFFFEu  /* std::numeric_limits<uint32_t>::max() - 1 (wharfmh.h:282) */
 
@@ -115,7 +116,9 @@ int wharf_generate(wharf_handle* h);
  * when WHARF_APPLY_WALK_UPDATES is set, by batch_walk_update (733-923).
  * pairs: m (src, dst) u32 pairs.  affected_out (may be NULL) receives the
  * affected walk ids in ascending order (the reference returns them in hash
- * order); capacity >= the owned walk count.  *n_affected receives the count. */
+ * order); capacity >= the owned walk count.  *n_affected receives the count.
+ * With WHARF_AFFECTED_DEVICE, affected_out is a device pointer and the ids
+ * stay in HBM (the call still returns after the update completed). */
 int wharf_insert_edges(wharf_handle* h, uint64_t m, const uint32_t* pairs, uint32_t flags,
                        uint32_t* affected_out, uint64_t* n_affected);
 int wharf_delete_edges(wharf_handle* h, uint64_t m, const uint32_t* pairs, uint32_t flags,

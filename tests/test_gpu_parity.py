@@ -224,6 +224,33 @@ def test_rmat_scale14_stream_vs_oracle(W):
     _compare_stream(W, off, adj, batches, wpv=10, L=80)
 
 
+def test_affected_ids_on_device_match_host_list(W):
+    """WHARF_AFFECTED_DEVICE: ids written to HBM equal the host list and the oracle's."""
+    import torch
+    base = O.generate_batch_of_edges(60000, 1 << 13, 9, False, False)
+    off, adj = O.csr_from_edges(1 << 13, base)
+    cfg = W.WharfConfig(walks_per_vertex=3, walk_length=30, deterministic=False, seed=7)
+    gh = W.WharfMH.from_csr(off, adj, config=cfg)
+    gd = W.WharfMH.from_csr(off, adj, config=cfg)
+    ref = O.Engine(off, adj, wpv=3, L=30, deterministic=False, seed=7)
+    gh.generate_initial_random_walks()
+    gd.generate_initial_random_walks()
+    ref.generate()
+    dout = torch.full((gd.number_of_walks,), -1, dtype=torch.int32, device="cuda:0")
+    for s, ins in ((1, True), (2, False)):
+        b = O.generate_batch_of_edges(1000, 1 << 13, s, False, False)
+        fl = O.REMOVE_DUPS | O.APPLY_WALK_UPDATES
+        ah = (gh.insert_edges_batch if ins else gh.delete_edges_batch)(b, remove_dups=True)
+        ad = (gd.insert_edges_batch if ins else gd.delete_edges_batch)(b, remove_dups=True, out=dout)
+        ar = ref.update(ins, b, fl)
+        assert ad.is_cuda and len(ad) == len(ah) > 0
+        assert np.array_equal(ad.cpu().numpy().view(np.uint32), ah)
+        np.testing.assert_array_equal(ah, ar)
+    assert np.array_equal(gd.walks(), ref.walks())
+    gh.destroy()
+    gd.destroy()
+
+
 # ---------------------------------------------------------------------------
 # MH mode
 # ---------------------------------------------------------------------------
