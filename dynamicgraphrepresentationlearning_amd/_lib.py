@@ -51,6 +51,11 @@ class wharf_stats(C.Structure):
     ]
 
 
+class wharf_memory(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("n", "m", "csr_bytes", "records_bytes", "walks_bytes", "samplers_bytes",
+                                          "edge_hash_bytes", "update_buffers_bytes", "scratch_bytes", "total_bytes")]
+
+
 # every symbol declared in include/wharf_gpu.h, with its ctypes signature
 _P, _U64, _U32, _I = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
 SIGNATURES = {
@@ -80,6 +85,7 @@ SIGNATURES = {
     "wharf_index_size": (_I, [_P, _P]),
     "wharf_export_index": (_I, [_P, _P, _P, _P]),
     "wharf_get_stats": (_I, [_P, _P]),
+    "wharf_memory_footprint": (_I, [_P, _P]),
     "wharf_generate_batch_of_edges": (_I, [_I, _U64, _U64, _U64, _I, _I, C.c_double, C.c_double, C.c_double, _P, _P]),
     "wharf_szudzik64": (_I, [_I, _I, _U64, _P, _P, _P]),
     "wharf_read_adjacency_graph": (_I, [C.c_char_p, _P, _P, _P, _P]),

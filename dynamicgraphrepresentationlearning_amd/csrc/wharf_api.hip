@@ -44,11 +44,15 @@ struct WharfError : std::runtime_error {
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
-    void ensure(size_t bytes)
+    // slack: growing buffers (the CSR double buffers of the batch merge) get
+    // 1/16 headroom, so a stream of insert batches does not free and re-map
+    // multi-GB buffers at every batch (measured: seconds per batch at 2.4 G edges)
+    void ensure(size_t bytes, bool slack = false)
     {
         if (bytes <= cap && p) return;
         release();
         size_t b = std::max<size_t>(bytes, 256);
+        if (slack) b += b / 16;
         HIPCHK(hipMalloc(&p, b));
         cap = b;
     }
@@ -87,7 +91,7 @@ struct wharf_handle {
     DevBuf off, adj, vrec, erec, anchor, row_epoch, off2, adj2, anchor2, ehash, erec2;
     uint64_t ehash_mask = 0, ehash_used = 0;   // capacity - 1; occupied slots incl. tombstones
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
-    DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, rtabs, count, pairs, sel;
+    DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, rtabs, count, pairs, sel, defer;
     wharf_stats st{};
     std::string err;
 
@@ -304,7 +308,7 @@ void free_handle(wharf_handle* h)
     if (h->s) (void)hipStreamSynchronize(h->s);
     for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->anchor, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
                       &h->aff, &h->rtab, &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags,
-                      &h->chg, &h->cf, &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel})
+                      &h->chg, &h->cf, &h->runstart, &h->runs, &h->rtabs, &h->count, &h->pairs, &h->sel, &h->defer})
         b->release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -335,6 +339,18 @@ void rmat_keys(wharf_handle* h, uint64_t edges_number, uint64_t vertices_number,
     h->k1.ensure(std::max<uint64_t>(total, 1) * 8);
     h->k2.ensure(std::max<uint64_t>(total, 1) * 8);
     launch_rmat_keys(p, edges_number, directed, h->k1.as<uint64_t>(), h->s);
+}
+
+// node2vec MH: affected walks a wave needs to re-walk them in place
+// (lock-step sweep, full-row stores); sparser waves defer theirs to the
+// compacted list kernel.  WHARF_LOCKSTEP_MIN: 0 = never defer, 65 = always.
+// (DeepWalk / deterministic steps are cheap enough that the sweep wins at
+// every density measured: configs[3] with 32 % of walks affected, 233 ms
+// swept vs 372 ms deferred.)
+uint32_t lockstep_min()
+{
+    const char* e = getenv("WHARF_LOCKSTEP_MIN");
+    return e ? (uint32_t)std::max(0, atoi(e)) : 40u;
 }
 
 int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, uint32_t flags,
@@ -408,8 +424,8 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         launch_run_info(bkeys, h->runstart.as<uint32_t>(), k, mb, h->off.as<uint64_t>(), h->runs.as<RunInfo>(),
                         h->bitmap.as<uint32_t>(), h->row_epoch.as<uint32_t>(), h->epoch, s);
         h->off2.ensure((h->n + 1) * 8);
-        h->adj2.ensure(std::max<uint64_t>(m_new, 1) * 4);
-        if (h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8);
+        h->adj2.ensure(std::max<uint64_t>(m_new, 1) * 4, true);
+        if (h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8, true);
         RunIndex rx;
         h->rtabs.ensure(run_tables_words(h->n, h->m) * 4);
         launch_run_tables(h->runs.as<RunInfo>(), k, h->n, h->m, h->rtabs.as<uint32_t>(), &rx, s);
@@ -418,7 +434,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         // a second record buffer fits; otherwise they are rebuilt by a gather
         bool patch = true;
         try {
-            h->erec2.ensure(std::max<uint64_t>(m_new, 1) * sizeof(ERec));
+            h->erec2.ensure(std::max<uint64_t>(m_new, 1) * sizeof(ERec), true);
         } catch (const WharfError&) {
             (void)hipGetLastError();
             patch = false;
@@ -460,10 +476,15 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         // 5. rewalk points + suffix re-walk in one pass over the walk matrix
         //    (wharfmh.h:519-537 and batch_walk_update 733-923)
         if (h->has_walks && h->W) {
-            HIPCHK(hipMemsetAsync(h->counters.p, 0, 16, s));
+            HIPCHK(hipMemsetAsync(h->counters.p, 0, 24, s));
             WalkArgs a = h->walk_args();
-            HIPCHK(hipEventRecord(h->ev[2], s));
             a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
+            a.lockstep_min = lockstep_min();
+            if (!a.scan_only && a.lockstep_min > 0 && a.model == kNode2Vec && !a.det) {   // k_rewalk_list
+                h->defer.ensure(h->W * 8);
+                a.defer = h->defer.as<uint64_t>();
+            }
+            HIPCHK(hipEventRecord(h->ev[2], s));
             launch_walk(a, true, s);
             HIPCHK(hipEventRecord(h->ev[3], s));
             // ascending affected walk ids
@@ -675,6 +696,7 @@ int wharf_set_shard(wharf_handle* h, uint64_t lo, uint64_t hi)
         h->sync();
         h->walks.release();
         h->aff.release();
+        h->defer.release();
         h->lo = lo;
         h->hi = hi;
         h->n_loc = hi - lo;
@@ -902,6 +924,27 @@ int wharf_export_index(wharf_handle* h, uint64_t* counts, uint64_t* keys, uint32
         HIPCHK(hipMemcpyAsync(counts, h->runs.p, h->n * 8, hipMemcpyDeviceToHost, h->s));
         h->sync();
     });
+}
+
+int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
+{
+    if (!h || !out) return WHARF_E_INVALID;
+    wharf_memory r{};
+    r.n = h->n;
+    r.m = h->m;
+    r.csr_bytes = h->off.cap + h->adj.cap;
+    r.records_bytes = h->vrec.cap + h->erec.cap;
+    r.walks_bytes = h->walks.cap + h->aff.cap;
+    r.samplers_bytes = h->anchor.cap + h->row_epoch.cap;
+    r.edge_hash_bytes = h->ehash.cap;
+    r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->anchor2.cap + h->erec2.cap;
+    r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
+                      h->runs.cap + h->rtabs.cap + h->count.cap + h->pairs.cap + h->sel.cap + h->defer.cap + h->rtab.cap +
+                      h->bitmap.cap + h->counters.cap + h->errflag.cap;
+    r.total_bytes = r.csr_bytes + r.records_bytes + r.walks_bytes + r.samplers_bytes + r.edge_hash_bytes +
+                    r.update_buffers_bytes + r.scratch_bytes;
+    *out = r;
+    return WHARF_OK;
 }
 
 int wharf_get_stats(const wharf_handle* h, wharf_stats* out)

@@ -32,6 +32,8 @@ struct WalkArgs {
     float inv_p, inv_q;
     int model, init, det;
     int scan_only;               // re-walk: only find rewalk points (apply_walk_updates=false)
+    uint64_t* defer;             // re-walk: walks of sparse waves, {li | p << 56}, count in counters[2]
+    uint32_t lockstep_min;       // re-walk: a wave with fewer affected walks defers them to `defer`
 };
 
 struct RunInfo {

@@ -235,20 +235,22 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
     wave_add(a.counters + 1, accepts);
 }
 
-// Fused rewalk-point scan + suffix re-walk (wharfmh.h:519-537 + 761-859).
-// The rewalk point of a walk is the first position holding a batch source;
-// positions after it are re-sampled on the updated graph.  Rewalk points
-// differ from lane to lane, so a lane-at-its-own-pace loop would make every
-// store of a wave hit 64 different rows (4-B partial-line writes, measured
-// 1.4x slower).  Instead each wave sweeps positions in lock step: at
-// position pos a lane is still scanning (reads the old value, checks the
-// bitmap), walking (writes a new vertex) or done; whenever any lane of the
-// wave writes, all lanes write (scanning lanes their old value), so each row
-// of a wave is one full 256-B store.
+// Fused rewalk-point scan + suffix re-walk (wharfmh.h:519-537 + 761-859),
+// DeepWalk and deterministic mode.  The rewalk point of a walk is the first
+// position holding a batch source; positions after it are re-sampled on the
+// updated graph.  Rewalk points differ from lane to lane, so a
+// lane-at-its-own-pace loop would make every store of a wave hit 64 different
+// rows (4-B partial-line writes, measured 1.4x slower).  Instead each wave
+// sweeps positions in lock step, scan and walk interleaved: at position pos a
+// lane is still scanning (reads the old value, checks the bitmap), walking
+// (writes a new vertex) or done; whenever any lane of the wave writes, all
+// lanes write (scanning lanes their old value), so each row of a wave is one
+// full 256-B store.  A lane starting its walk costs the wave one 16-B gather,
+// so the scan of late-starting lanes hides behind the walking of the others.
 enum : uint32_t { kLaneScan = 0, kLaneWalk = 1, kLaneDone = 2 };
 
 template <int MODEL, bool DET>
-__global__ __launch_bounds__(256) void k_rewalk(WalkArgs a)
+__global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
 {
     uint32_t steps = 0, accepts = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -308,6 +310,154 @@ __global__ __launch_bounds__(256) void k_rewalk(WalkArgs a)
     wave_add(a.counters + 1, accepts);
 }
 
+// Fused rewalk-point scan + suffix re-walk, node2vec MH.  Setting up a
+// node2vec walker is a chain of dependent loads (rows of cur and prev, the
+// binary search for the anchor-cache slot of the edge prev -> cur), which
+// would stall the interleaved sweep once per distinct rewalk point of the
+// wave.  Three phases per wave instead:
+//   A. each lane scans its old walk (coalesced row reads, bitmap test) up to
+//      its rewalk point or the walk's end;
+//   B. every affected lane builds its walker state (rows of cur / prev, the
+//      node2vec anchor-cache slot) — one dependent chain for the whole wave;
+//   C. the wave sweeps positions from its smallest rewalk point in lock step:
+//      walking lanes write new vertices, the others re-write the old value
+//      they read, so every row of a wave is one full 256-B store.  Rewalk
+//      points differ from lane to lane; a lane-at-its-own-pace loop would make
+//      each store instruction hit up to 64 rows with 4-B partial-line writes
+//      (measured 1.4x slower on configs[2]).
+template <int MODEL, bool DET>
+__global__ __launch_bounds__(256) void k_rewalk(WalkArgs a)
+{
+    uint32_t steps = 0, accepts = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t* __restrict__ walks = a.walks;
+    const uint64_t W = a.W;
+    const uint32_t L = a.L;
+    for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += stride) {
+        const uint64_t r = li / a.n_loc;
+        const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
+        const uint64_t wid = r * a.n + v;
+        const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
+        const uint64_t* __restrict__ rt = DET ? a.rtab + r * L : nullptr;
+        // A. scan
+        uint32_t p = kNoRewalk, x = v, xprev = v;
+        uint32_t xn = L > 1 ? walks[W + li] : kSent;   // next position, prefetched
+        for (uint32_t pos = 0; pos < L; pos++) {
+            if (pos > 0) {
+                xprev = x;
+                x = xn;
+                if (x == kSent) break;
+                if (pos + 1 < L) xn = walks[(uint64_t)(pos + 1) * W + li];
+            }
+            if ((a.bitmap[x >> 5] >> (x & 31)) & 1u) { p = pos; break; }
+        }
+        a.aff[li] = (uint8_t)p;
+        if (a.scan_only) continue;
+        const bool active = p + 1 < L;   // affected, and something after the rewalk point
+        if (a.defer) {
+            // A wave with few affected walks would sweep with most lanes idle:
+            // hand its walks to k_rewalk_list (one atomic per wave) instead.
+            const uint64_t mask = __ballot(active);
+            const uint32_t cnt = (uint32_t)__popcll(mask);
+            if (cnt == 0) continue;
+            if (cnt < a.lockstep_min) {
+                const uint32_t lane = __lane_id(), leader = (uint32_t)__ffsll((long long)mask) - 1;
+                unsigned long long base = 0;
+                if (lane == leader) base = atomicAdd(a.counters + 2, (unsigned long long)cnt);
+                base = __shfl(base, (int)leader, 64);
+                if (active) a.defer[base + __popcll(mask & ((1ull << lane) - 1))] = li | ((uint64_t)p << 56);
+                continue;
+            }
+        }
+        // B. walker state at the rewalk point
+        Row rc, rp;
+        rc.deg = 0;
+        int64_t ein = -1;
+        if (active) walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, rc, rp, ein);
+        // C. lock-step sweep from the wave's smallest rewalk point
+        uint32_t first = active ? p + 1 : L;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, o, 64));
+        for (uint32_t pos = first; pos < L; pos++) {
+            const uint64_t at = (uint64_t)pos * W + li;
+            uint32_t val;
+            if (active && pos > p) {
+                val = kSent;
+                if (rc.deg) {
+                    const Row nx = walk_step<MODEL, DET>(a, rc, rp, ein, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep,
+                                                         accepts);
+                    val = nx.v;
+                    steps++;
+                    rp = rc;
+                    rc = nx;
+                }
+            } else {
+                val = walks[at];   // not (yet) re-walking: keep the old value
+            }
+            walks[at] = val;
+        }
+    }
+    wave_add(a.counters + 0, steps);
+    wave_add(a.counters + 1, accepts);
+}
+
+// Re-walk of the deferred walks (sparse waves of k_rewalk): a compacted list,
+// lanes at their own pace.  One flattened loop — a lane whose walk is done
+// takes its next list entry in the same iteration instead of waiting for the
+// rest of its wave.  Stores land in scattered rows (partial lines), the price
+// of keeping every lane busy; results are identical to the lock-step sweep
+// (each walk's draws depend only on its id, positions and the epoch).
+template <int MODEL, bool DET>
+__global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
+{
+    uint32_t steps = 0, accepts = 0;
+    const uint64_t cnt = a.counters[2];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t* __restrict__ walks = a.walks;
+    const uint64_t W = a.W;
+    const uint32_t L = a.L, ep = a.epoch << 4;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t li = 0;
+    uint32_t p = 0, pos = L, wlo = 0, whi = 0;
+    const uint64_t* __restrict__ rt = nullptr;
+    Row rc, rp;
+    rc.deg = 0;
+    int64_t ein = -1;
+    for (;;) {
+        if (pos >= L && i < cnt) {   // next walk of this lane
+            const uint64_t e = a.defer[i];
+            i += stride;
+            li = e & ((1ull << 56) - 1);
+            p = (uint32_t)(e >> 56);
+            const uint64_t r = li / a.n_loc;
+            const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
+            wlo = (uint32_t)wid;
+            whi = (uint32_t)(wid >> 32);
+            if constexpr (DET) rt = a.rtab + r * L;
+            const uint32_t x = walks[(uint64_t)p * W + li];
+            const uint32_t xprev = p ? walks[(uint64_t)(p - 1) * W + li] : x;
+            walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, rc, rp, ein);
+            pos = p + 1;
+        }
+        if (!__any(pos < L)) break;
+        if (pos < L) {
+            uint32_t val = kSent;
+            if (rc.deg) {
+                const Row nx = walk_step<MODEL, DET>(a, rc, rp, ein, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep,
+                                                     accepts);
+                val = nx.v;
+                steps++;
+                rp = rc;
+                rc = nx;
+            }
+            walks[(uint64_t)pos * W + li] = val;
+            pos++;
+        }
+    }
+    wave_add(a.counters + 0, steps);
+    wave_add(a.counters + 1, accepts);
+}
+
 // Blocks for the walk kernels: one walk per lane by default; a smaller grid of
 // lanes each looping over several walks with WHARF_WALK_BLOCKS_PER_CU=k
 // (k blocks of 256 per CU; 0 = one walk per lane).
@@ -326,14 +476,33 @@ static unsigned walk_grid(uint64_t W)
     return (unsigned)std::min<uint64_t>(full, (uint64_t)cus * per_cu);
 }
 
+// resident lanes for the deferred-walk list kernel (8 blocks of 256 per CU)
+static unsigned list_grid()
+{
+    static int cus = -1;
+    if (cus < 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    return (unsigned)cus * 8;
+}
+
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
 {
     if (a.W == 0) return;
     const dim3 grid(walk_grid(a.W)), block(256);
-#define WHARF_LAUNCH(M, D)                                                        \
-    do {                                                                          \
-        if (rewalk) hipLaunchKernelGGL((k_rewalk<M, D>), grid, block, 0, s, a);   \
-        else hipLaunchKernelGGL((k_walk<M, D>), grid, block, 0, s, a);            \
+    const dim3 lgrid(list_grid());
+#define WHARF_LAUNCH(M, D)                                                                   \
+    do {                                                                                     \
+        if (rewalk && M == kNode2Vec) {                                                      \
+            hipLaunchKernelGGL((k_rewalk<M, D>), grid, block, 0, s, a);                      \
+            if (a.defer && !a.scan_only) hipLaunchKernelGGL((k_rewalk_list<M, D>), lgrid, block, 0, s, a); \
+        } else if (rewalk) {                                                                 \
+            hipLaunchKernelGGL((k_rewalk_sweep<M, D>), grid, block, 0, s, a);                \
+        } else {                                                                             \
+            hipLaunchKernelGGL((k_walk<M, D>), grid, block, 0, s, a);                        \
+        }                                                                                    \
     } while (0)
     if (a.det) WHARF_LAUNCH(kDeepWalk, true);
     else if (a.model == kDeepWalk) WHARF_LAUNCH(kDeepWalk, false);

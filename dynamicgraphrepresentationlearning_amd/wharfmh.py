@@ -155,6 +155,22 @@ class WharfMH:
         L.check(L.lib.wharf_get_stats(self._h, C.byref(s)), self._h, "stats")
         return {k: getattr(s, k) for k, _ in L.wharf_stats._fields_}
 
+    def memory_footprint(self, verbose: bool = True) -> dict:
+        """WharfMH::memory_footprint (wharfmh.h:928-998): device bytes by role
+        (printed like the reference when verbose)."""
+        r = L.wharf_memory()
+        L.check(L.lib.wharf_memory_footprint(self._h, C.byref(r)), self._h, "memory_footprint")
+        d = {f: getattr(r, f) for f, _ in r._fields_}
+        if verbose:
+            gb = lambda b: f"{b / 2**20:.2f} MB = {b / 2**30:.3f} GB"
+            print(f"\nGraph: \n\tVertices: {d['n']}, Edges: {d['m']}")
+            for k, name in (("csr_bytes", "CSR"), ("records_bytes", "Row records"), ("walks_bytes", "Walks"),
+                            ("samplers_bytes", "Samplers"), ("edge_hash_bytes", "Edge hash"),
+                            ("update_buffers_bytes", "Update buffers"), ("scratch_bytes", "Scratch")):
+                print(f"{name}: \n\tMemory usage: {gb(d[k])}")
+            print(f"Total memory used: \n\t{gb(d['total_bytes'])}\n")
+        return d
+
     def flatten_graph(self):
         n, m = self.number_of_vertices(), self.number_of_edges()
         off = np.zeros(n + 1, dtype=np.uint64)

@@ -164,6 +164,22 @@ int wharf_export_index(wharf_handle* h, uint64_t* counts, uint64_t* keys, uint32
 
 int wharf_get_stats(const wharf_handle* h, wharf_stats* out);
 
+/* WharfMH::memory_footprint (wharfmh.h:928-998), which prints the bytes of the
+ * vertex tree, edge C-trees, walk trees and samplers: here the device bytes
+ * held by the handle, by role. */
+typedef struct wharf_memory {
+    uint64_t n, m;
+    uint64_t csr_bytes;             /* offsets + targets (the edge trees' content) */
+    uint64_t records_bytes;         /* vertex + edge row records */
+    uint64_t walks_bytes;           /* walk matrix + per-walk rewalk positions (the walk trees) */
+    uint64_t samplers_bytes;        /* MH anchors + per-row sampler epochs (the samplers) */
+    uint64_t edge_hash_bytes;       /* node2vec has_edge set */
+    uint64_t update_buffers_bytes;  /* second CSR / record buffers of the batch merge */
+    uint64_t scratch_bytes;         /* sort / select temporaries, batch and draw tables */
+    uint64_t total_bytes;
+} wharf_memory;
+int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out);
+
 /* utility::generate_batch_of_edges (utils/utility.h:55-146) on the device:
  * sorted, deduplicated (src,dst) pairs.  out_pairs capacity: 2*edges_number
  * pairs when undirected, edges_number otherwise. */

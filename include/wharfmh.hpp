@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <iostream>
 #include <stdexcept>
 #include <string>
 #include <tuple>
@@ -157,6 +158,22 @@ public:
         wharf_stats s{};
         check(wharf_get_stats(h_, &s), h_, "stats");
         return s;
+    }
+    // WharfMH::memory_footprint (wharfmh.h:928-998): prints the device bytes by role
+    wharf_memory memory_footprint() const
+    {
+        wharf_memory r{};
+        check(wharf_memory_footprint(h_, &r), h_, "memory_footprint");
+        auto mb = [](uint64_t b) { return std::to_string(b / 1048576.0) + " MB = " + std::to_string(b / 1073741824.0) + " GB"; };
+        std::cout << "\nGraph: \n\tVertices: " << r.n << ", Edges: " << r.m << "\n"
+                  << "CSR: \n\tMemory usage: " << mb(r.csr_bytes) << "\n"
+                  << "Row records: \n\tMemory usage: " << mb(r.records_bytes) << "\n"
+                  << "Walks: \n\tMemory usage: " << mb(r.walks_bytes) << "\n"
+                  << "Samplers: \n\tMemory usage: " << mb(r.samplers_bytes) << "\n"
+                  << "Edge hash: \n\tMemory usage: " << mb(r.edge_hash_bytes) << "\n"
+                  << "Total memory used: \n\t" << mb(r.total_bytes) << "\n"
+                  << std::endl;
+        return r;
     }
     wharf_handle* handle() const { return h_; }
 

@@ -103,6 +103,9 @@ static void test_destroy(const Csr& g)
     std::vector<uint32_t> nx;
     w.inverted_index(c, k, nx);
     EXPECT(!k.empty());
+    const wharf_memory mem = w.memory_footprint();   // memory-footprint.cpp's report
+    EXPECT(mem.n == g.n && mem.m == g.m && mem.walks_bytes >= k.size() * 4 && mem.csr_bytes >= g.m * 4);
+    EXPECT(mem.total_bytes >= mem.csr_bytes + mem.records_bytes + mem.walks_bytes);
     w.destroy_index();
     w.inverted_index(c, k, nx);
     EXPECT(k.empty());

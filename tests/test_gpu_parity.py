@@ -247,8 +247,28 @@ def test_affected_ids_on_device_match_host_list(W):
         assert np.array_equal(ad.cpu().numpy().view(np.uint32), ah)
         np.testing.assert_array_equal(ah, ar)
     assert np.array_equal(gd.walks(), ref.walks())
+    mem = gd.memory_footprint(verbose=False)
+    assert mem["walks_bytes"] >= gd.number_of_walks * 30 * 4 and mem["csr_bytes"] >= gd.number_of_edges() * 4
     gh.destroy()
     gd.destroy()
+
+
+@pytest.mark.parametrize("lockstep_min", ["0", "65"])
+@pytest.mark.parametrize("mode", ["det", "deepwalk", "node2vec"])
+def test_rewalk_paths_lockstep_and_deferred(W, monkeypatch, lockstep_min, mode):
+    """Every re-walk kernel reproduces the oracle's corpus, counters and affected
+    ids: the interleaved sweep (DeepWalk, deterministic), and for node2vec the
+    phased sweep (WHARF_LOCKSTEP_MIN=0) and the compacted deferred list (=65:
+    every wave defers)."""
+    monkeypatch.setenv("WHARF_LOCKSTEP_MIN", lockstep_min)
+    base = O.generate_batch_of_edges(50000, 1 << 13, 6, False, False)
+    off, adj = O.csr_from_edges(1 << 12, base)
+    batches = [(True, O.generate_batch_of_edges(800, 1 << 12, 11, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
+               (False, O.generate_batch_of_edges(600, 1 << 12, 12, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
+               (True, O.generate_batch_of_edges(40, 1 << 12, 13, False, True), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES)]
+    kw = dict(deterministic=True) if mode == "det" else dict(
+        deterministic=False, seed=99, model=1 if mode == "node2vec" else 0, paramP=0.5, paramQ=2.0)
+    _compare_stream(W, off, adj, batches, wpv=3, L=40, **kw)
 
 
 # ---------------------------------------------------------------------------

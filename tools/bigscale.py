@@ -1,14 +1,21 @@
 #!/usr/bin/env python3
-"""Maximum-size check on one MI355X: the configs[4] (com-friendster-sized) graph.
+"""Full-size runs of the large configs on ONE MI355X (288 GB HBM).
 
-RMAT scale 26 (67.1 M vertices), 1.8 G undirected samples -> m >= 2^32 CSR
-entries (exercises the 64-bit CSR offsets / 40-bit record offsets), built on the
-device.  One walk per vertex (the 10-walk corpus of this graph does not fit one
-GPU next to the graph; on 8 GPUs each holds 1/8 of it).  Checks: step counts,
-every sampled transition is an edge, a window of walks re-computed by the
-oracle, one 10k-edge insert + delete with affected walks cross-checked.
+configs[4] (com-friendster-sized, default): RMAT scale 26 (67.1 M vertices),
+1.8 G undirected samples -> 3.6 G CSR entries, built on the device.  One walk
+per vertex with node2vec (the anchors and the edge hash take the room of the
+other nine), ten with DeepWalk only at scale 25.
 
-    python tools/bigscale.py [--scale 26 --samples 1800000000 --model deepwalk]
+configs[3] (twitter-sized): --scale 25 --samples 1200000000 --wpv 10
+--batches 50: 335 M walks (107 GB walk matrix, 26.5 G stored positions)
+next to a 2.4 G-entry CSR, initial generation + 50 insert batches.
+
+Checks: step counts, every sampled transition is an edge, a window of walks
+re-computed by the oracle (DeepWalk), the walk ids of insert batches, a
+delete of the last batch restoring m.  --mixed alternates insert b / delete b
+(throughput-latency.cpp:126,135).
+
+    python tools/bigscale.py [--scale 26 --samples 1800000000 --model deepwalk --wpv 1 --batches 1]
 """
 import argparse
 import json
@@ -28,7 +35,11 @@ def main():
     ap.add_argument("--samples", type=int, default=1_800_000_000)
     ap.add_argument("--model", default="deepwalk")
     ap.add_argument("--wpv", type=int, default=1)
+    ap.add_argument("--batches", type=int, default=1)
+    ap.add_argument("--mixed", action="store_true", help="insert batch b, then delete it")
+    ap.add_argument("--no-oracle", action="store_true")
     a = ap.parse_args()
+    import torch
     import dynamicgraphrepresentationlearning_amd as W
     from oracle import oracle as O
 
@@ -41,7 +52,7 @@ def main():
     g = W.WharfMH.from_rmat(n, a.samples, 2 * n, seed=4, config=cfg)
     m = g.number_of_edges()
     t_build = time.time() - t0
-    print(f"graph n={n} m={m} (m >= 2^32: {m >= 2**32}) built in {t_build:.1f}s", flush=True)
+    print(f"graph n={n} m={m} built in {t_build:.1f}s", flush=True)
     g.generate_initial_random_walks()
     g.generate_initial_random_walks()
     st = g.stats()
@@ -49,11 +60,16 @@ def main():
     deg = np.diff(off.astype(np.int64))
     active = int((deg > 0).sum()) * a.wpv
     ok_steps = st["steps"] == active * 79
+    gen_rate = st["steps"] / st["last_walk_kernel_ms"] / 1e6
     print(f"generate: {st['last_walk_kernel_ms']:.1f} ms, steps {st['steps']} (expected {active * 79}), "
-          f"{st['steps'] / st['last_walk_kernel_ms'] / 1e6:.2f} G steps/s", flush=True)
+          f"{gen_rate:.2f} G steps/s, accepts {st['accepts']}", flush=True)
+    mem = g.memory_footprint(verbose=False)
+    free, total = torch.cuda.mem_get_info(0)
+    print(f"device bytes: {json.dumps(mem)}; hipMemGetInfo free {free / 2**30:.1f} of {total / 2**30:.1f} GiB",
+          flush=True)
     # sampled transitions are edges
     rng = np.random.default_rng(1)
-    wids = rng.choice(n * a.wpv, 2000, replace=False)
+    wids = rng.choice(g.number_of_walks, 2000, replace=False)
     bad = 0
     for w in wids:
         v = g.walk_vertices(int(w))
@@ -63,10 +79,9 @@ def main():
             bad += not (j < len(row) and row[j] == y)
     print(f"sampled transitions not in the graph: {bad}", flush=True)
     # oracle re-computes a window of walks on the same (downloaded) CSR
-    w0 = int(off.size // 3)
-    ref = None
     same = None
-    if not node2vec:
+    if not node2vec and not a.no_oracle:
+        w0 = int(n // 3)
         ref = O.Engine(off, adj, wpv=a.wpv, L=80, deterministic=False, seed=11)
         ref.time_generate_range(w0, w0 + 2048)
         mine = np.stack([np.pad(g.walk_vertices(w), (0, 80 - len(g.walk_vertices(w))), constant_values=W.SENTINEL)
@@ -74,23 +89,45 @@ def main():
         same = bool(np.array_equal(mine, ref.walks()[w0:w0 + 2048]))
         print(f"oracle window [{w0}, {w0 + 2048}) identical: {same}", flush=True)
         del ref
-    b = W.generate_batch_of_edges(5000, n, 0, False, False)
-    t1 = time.time()
-    aff = g.insert_edges_batch(b, remove_dups=True)
-    s2 = g.stats()
-    print(f"insert 10k edges: {(time.time() - t1) * 1e3:.1f} ms wall, graph {s2['last_graph_update_ms']:.1f} ms, "
-          f"re-walk {s2['last_walk_update_ms']:.1f} ms, affected {len(aff)}", flush=True)
+    del off, adj, deg
+    out = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device="cuda:0")
+    lat, gms, wms, affs, steps = [], [], [], [], []
+    for b in range(a.batches):
+        batch = W.generate_batch_of_edges(5000, n, b, False, False)
+        for ins in ((True, False) if a.mixed else (True,)):
+            t1 = time.perf_counter()
+            aff = (g.insert_edges_batch if ins else g.delete_edges_batch)(batch, remove_dups=True, out=out)
+            lat.append((time.perf_counter() - t1) * 1e3)
+            s2 = g.stats()
+            gms.append(s2["last_graph_update_ms"])
+            wms.append(s2["last_walk_update_ms"])
+            affs.append(len(aff))
+            steps.append(s2["steps"])
+        print(f"batch {b}: {lat[-1]:.1f} ms (graph {gms[-1]:.1f}, re-walk {wms[-1]:.1f}), affected {affs[-1]}, "
+              f"m {g.number_of_edges()}", flush=True)
+        if b == 0:
+            m1 = g.memory_footprint(verbose=False)
+            free, _ = torch.cuda.mem_get_info(0)
+            print(f"after batch 0: update buffers {m1['update_buffers_bytes'] / 2**30:.1f} GiB, scratch "
+                  f"{m1['scratch_bytes'] / 2**30:.1f} GiB, free {free / 2**30:.1f} GiB", flush=True)
     m2 = g.number_of_edges()
-    aff2 = g.delete_edges_batch(b, remove_dups=True)
-    print(f"delete: affected {len(aff2)}, m {m} -> {m2} -> {g.number_of_edges()}", flush=True)
-    res = {"n": n, "m": m, "m_ge_2^32": m >= 2 ** 32, "build_s": round(t_build, 1),
-           "gen_ms": round(st["last_walk_kernel_ms"], 2), "steps_ok": ok_steps, "bad_transitions": bad,
-           "oracle_window_identical": same, "insert_affected": int(len(aff)),
-           "insert_graph_ms": round(s2["last_graph_update_ms"], 2), "insert_rewalk_ms": round(s2["last_walk_update_ms"], 2),
-           "m_after_insert": m2, "m_after_delete": g.number_of_edges(), "hbm_bytes_graph": st["hbm_bytes_graph"],
-           "hbm_bytes_walks": st["hbm_bytes_walks"]}
+    last = W.generate_batch_of_edges(5000, n, a.batches - 1, False, False)
+    g.delete_edges_batch(last, remove_dups=True, out=out)
+    m3 = g.number_of_edges()
+    res = {"config": f"RMAT scale {a.scale}, {a.samples} undirected samples (seed 4), {a.model} MH, wpv {a.wpv}, "
+                     f"L 80, {a.batches} {'insert+delete' if a.mixed else 'insert'} batches of "
+                     "generate_batch_of_edges(5000, n, b, false, false)",
+           "n": n, "m": m, "walks": g.number_of_walks, "build_s": round(t_build, 1),
+           "gen_ms": round(st["last_walk_kernel_ms"], 2), "gen_Gsteps_per_s": round(gen_rate, 2),
+           "steps_ok": ok_steps, "bad_transitions": bad, "oracle_window_identical": same,
+           "batch_median_ms": round(float(np.median(lat)), 2), "batch_p90_ms": round(float(np.percentile(lat, 90)), 2),
+           "graph_update_median_ms": round(float(np.median(gms)), 2),
+           "walk_update_median_ms": round(float(np.median(wms)), 2),
+           "mean_affected": int(np.mean(affs)),
+           "rewalk_Gsteps_per_s": round(float(np.sum(steps) / np.sum(wms) / 1e6), 2),
+           "m_after_batches": m2, "m_after_delete_last": m3, "device_bytes_total": mem["total_bytes"]}
     print(json.dumps(res), flush=True)
-    assert ok_steps and bad == 0 and same in (True, None) and m2 >= m >= g.number_of_edges()
+    assert ok_steps and bad == 0 and same in (True, None) and m3 <= m2
     g.destroy()
 
 

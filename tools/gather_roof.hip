@@ -8,10 +8,15 @@
 //   dep    next slot depends on the loaded record (pointer chasing, like a walk)
 //   indep  slots from a counter hash (no dependency: max memory-level parallelism)
 //   stream the same bytes read sequentially (HBM streaming ceiling)
+//
+// Second argument: table memory kind — "coarse" (hipMalloc, default),
+// "uncached" (hipDeviceMallocUncached: requests bypass L2 line fills) or
+// "fine" (hipDeviceMallocFinegrained).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CHK(x)                                                                   \
@@ -81,7 +86,10 @@ int main(int argc, char** argv)
     const int L = 79;
     uint4* t;
     uint32_t* out;
-    CHK(hipMalloc(&t, n * 16));
+    const char* kind = argc > 2 ? argv[2] : "coarse";
+    if (!std::strcmp(kind, "uncached")) CHK(hipExtMallocWithFlags((void**)&t, n * 16, hipDeviceMallocUncached));
+    else if (!std::strcmp(kind, "fine")) CHK(hipExtMallocWithFlags((void**)&t, n * 16, hipDeviceMallocFinegrained));
+    else CHK(hipMalloc(&t, n * 16));
     CHK(hipMalloc(&out, W * L * 4));
     hipLaunchKernelGGL(k_init, 4096, 256, 0, 0, t, n);
     CHK(hipDeviceSynchronize());
@@ -103,9 +111,9 @@ int main(int argc, char** argv)
             CHK(hipEventElapsedTime(&ms, a, b));
             const double g = (double)W * L;
             if (rep == 1)
-                std::printf("{\"mode\": \"%s\", \"table_GiB\": %.2f, \"ms\": %.3f, \"Ggathers_per_s\": %.2f, "
+                std::printf("{\"mode\": \"%s\", \"mem\": \"%s\", \"table_GiB\": %.2f, \"ms\": %.3f, \"Ggathers_per_s\": %.2f, "
                             "\"useful_GBps_16B\": %.1f}\n",
-                            names[mode], gib, ms, g / ms / 1e6, g * 20 / ms / 1e6);
+                            names[mode], kind, gib, ms, g / ms / 1e6, g * 20 / ms / 1e6);
         }
     return 0;
 }

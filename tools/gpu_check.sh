@@ -25,8 +25,18 @@ for s in "$@"; do
     rwsweep) for b in 0 8 16 32 64; do
                step rw_bpc$b 600 env WHARF_WALK_BLOCKS_PER_CU=$b python bench.py --steps 2 --warmup 1 --rewalk-batches 10 --cpu-baseline off
              done ;;
+    lssweep) for t in 0 8 16 24 40 65; do
+               step ls_c3_dw_$t 300 env WHARF_LOCKSTEP_MIN=$t python tools/rewalk_probe.py --batches 3
+               step ls_c3_n2v_$t 300 env WHARF_LOCKSTEP_MIN=$t python tools/rewalk_probe.py --batches 3 --model node2vec
+             done
+             for t in 0 16 40 65; do
+               step ls_c4_$t 600 env WHARF_LOCKSTEP_MIN=$t python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 2 --no-oracle
+               step ls_c5_$t 600 env WHARF_LOCKSTEP_MIN=$t python tools/bigscale.py --model node2vec --wpv 1 --batches 2 --mixed
+             done ;;
     roof)   step gather_roof 300 tools/gather_roof 3.48 ;;
     big)    step bigscale 900 python tools/bigscale.py ;;
+    c4)     step c4_stream 1100 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 50 ;;
+    c5n2v)  step c5_node2vec 1100 python tools/bigscale.py --model node2vec --wpv 1 --batches 10 --mixed ;;
     det)    step bench_det 900 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     n2v)    step bench_n2v 900 python bench.py --model node2vec --steps 2 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     dist2)  step bench_dist2 900 env WHARF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --scale 20 --samples 29296270 --stream-samples 10000000 --steps 3 --warmup 1 --rewalk-batches 5 ;;
