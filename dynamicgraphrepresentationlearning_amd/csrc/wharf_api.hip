@@ -65,11 +65,6 @@ struct DevBuf {
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-struct NotNoRewalk {
-    const uint8_t* aff;
-    __device__ bool operator()(uint64_t li) const { return aff[li] != kNoRewalk; }
-};
-
 uint32_t bits_for(uint64_t x)   // bits needed to represent values < x
 {
     uint32_t b = 0;
@@ -134,7 +129,7 @@ struct wharf_handle {
     void csr_from_keys(uint64_t mm)
     {
         off.ensure((n + 1) * 8);
-        adj.ensure(std::max<uint64_t>(mm, 1) * 4);
+        adj.ensure(std::max<uint64_t>(mm, 1) * 4, true);   // slack: insert batches grow it in place
         launch_offsets_from_keys(k1.as<uint64_t>(), mm, n, off.as<uint64_t>(), s);
         launch_low32(k1.as<uint64_t>(), mm, adj.as<uint32_t>(), s);
         m = mm;
@@ -146,7 +141,7 @@ struct wharf_handle {
         HIPCHK(hipMemsetAsync(row_epoch.p, 0, std::max<uint64_t>(n, 1) * 4, s));
         build_records();
         if (anchors) {
-            anchor.ensure(std::max<uint64_t>(m, 1) * 8);
+            anchor.ensure(std::max<uint64_t>(m, 1) * 8, true);
             launch_fill_u64(anchor.as<uint64_t>(), m, kAnchorNone64, s);
         }
         bitmap.ensure(((n + 31) / 32 + 1) * 4);
@@ -168,7 +163,7 @@ struct wharf_handle {
     void build_records()
     {
         vrec.ensure(std::max<uint64_t>(n, 1) * sizeof(ERec));
-        erec.ensure(std::max<uint64_t>(m, 1) * sizeof(ERec));
+        erec.ensure(std::max<uint64_t>(m, 1) * sizeof(ERec), true);
         launch_vrec(off.as<uint64_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
         launch_erec(adj.as<uint32_t>(), m, vrec.as<ERec>(), erec.as<ERec>(), s);
         if (anchors) build_edge_hash();
@@ -428,7 +423,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         if (h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8, true);
         RunIndex rx;
         h->rtabs.ensure(run_tables_words(h->n, h->m) * 4);
-        launch_run_tables(h->runs.as<RunInfo>(), k, h->n, h->m, h->rtabs.as<uint32_t>(), &rx, s);
+        launch_run_tables(h->runs.as<RunInfo>(), k, h->cf.as<uint32_t>(), mb, h->n, h->m, h->rtabs.as<uint32_t>(), &rx, s);
         launch_new_offsets(h->off.as<uint64_t>(), h->n, rx, h->cf.as<uint32_t>(), mb, insert, h->off2.as<uint64_t>(), s);
         // edge records move with their slot and are patched arithmetically when
         // a second record buffer fits; otherwise they are rebuilt by a gather
@@ -487,25 +482,28 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             HIPCHK(hipEventRecord(h->ev[2], s));
             launch_walk(a, true, s);
             HIPCHK(hipEventRecord(h->ev[3], s));
-            // ascending affected walk ids
-            h->sel.ensure(h->W * 8);
-            h->pairs.ensure(h->W * 4);
-            auto cnt_it = rocprim::counting_iterator<uint64_t>(0);
-            uint64_t* out = h->sel.as<uint64_t>();
-            uint64_t* c = h->count.as<uint64_t>();
-            NotNoRewalk pred{h->aff.as<uint8_t>()};
-            h->rp([&](void* t, size_t& b) { return rocprim::select(t, b, cnt_it, out, c, (size_t)h->W, pred, s); });
-            uint64_t naff = 0;
-            HIPCHK(hipMemcpyAsync(&naff, c, 8, hipMemcpyDeviceToHost, s));
+            // ascending affected walk ids: count per block, scan, write
+            const unsigned nb = aff_blocks(h->W);
+            h->sel.ensure((uint64_t)(nb + 1) * 8);
+            uint32_t* bcount = h->sel.as<uint32_t>();
+            uint32_t* boff = bcount + nb + 1;
+            HIPCHK(hipMemsetAsync(bcount + nb, 0, 4, s));
+            launch_aff_count(h->aff.as<uint8_t>(), h->W, bcount, s);
+            h->rp([&](void* t, size_t& b) {
+                return rocprim::exclusive_scan(t, b, bcount, boff, 0u, (size_t)nb + 1, rocprim::plus<uint32_t>(), s);
+            });
+            const bool on_device = affected_out && (flags & WHARF_AFFECTED_DEVICE);
+            if (!on_device) h->pairs.ensure(h->W * 4);
+            launch_aff_write(h->aff.as<uint8_t>(), h->W, boff, h->n, h->n_loc, h->lo,
+                             on_device ? affected_out : h->pairs.as<uint32_t>(), s);
+            uint32_t naff32 = 0;
+            HIPCHK(hipMemcpyAsync(&naff32, boff + nb, 4, hipMemcpyDeviceToHost, s));
             h->sync();
-            if (affected_out && (flags & WHARF_AFFECTED_DEVICE)) {
-                launch_li_to_wid(out, naff, h->n, h->n_loc, h->lo, affected_out, s);
-            } else {
-                launch_li_to_wid(out, naff, h->n, h->n_loc, h->lo, h->pairs.as<uint32_t>(), s);
-                if (affected_out && naff)
-                    HIPCHK(hipMemcpyAsync(affected_out, h->pairs.p, naff * 4, hipMemcpyDeviceToHost, s));
+            const uint64_t naff = naff32;
+            if (affected_out && !on_device && naff) {
+                HIPCHK(hipMemcpyAsync(affected_out, h->pairs.p, naff * 4, hipMemcpyDeviceToHost, s));
+                h->sync();
             }
-            h->sync();
             h->st.affected = naff;
             if (n_affected) *n_affected = naff;
             h->read_counters();

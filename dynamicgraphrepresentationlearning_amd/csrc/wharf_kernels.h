@@ -45,8 +45,9 @@ struct RunInfo {
 struct RunIndex {
     const RunInfo* runs;
     uint64_t k;
-    const uint32_t* vtab;   // [(n >> vs) + 2]
+    const uint2* vtab;      // [(n >> vs) + 2] {first run, row shift}
     const uint32_t* etab;   // [(m >> es) + 2]
+    const uint32_t* eshift; // [(m >> es) + 2] clean bucket: 1 << 31 | shift of its slots, else 0
     uint32_t vs, es;
 };
 // bucket shift so a table over [0, x] has at most ~2^target entries
@@ -58,10 +59,11 @@ inline uint32_t run_table_shift(uint64_t x, uint32_t target)
 }
 inline uint64_t run_tables_words(uint64_t n, uint64_t m)
 {
-    return (n >> run_table_shift(n, 18)) + 2 + (m >> run_table_shift(m, 20)) + 2;
+    return 2 * ((n >> run_table_shift(n, 18)) + 2) + 2 * ((m >> run_table_shift(m, 20)) + 2);
 }
 
 unsigned grid_for(uint64_t work, unsigned block);
+unsigned cu_count();
 
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s);
 void launch_vrec(const uint64_t* off, uint64_t n, const uint32_t* row_epoch, ERec* vrec, hipStream_t s);
@@ -77,8 +79,8 @@ void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off
 void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_t s);
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
                      RunInfo* runs, uint32_t* bitmap, uint32_t* row_epoch, uint32_t epoch, hipStream_t s);
-void launch_run_tables(const RunInfo* runs, uint64_t k, uint64_t n, uint64_t m, uint32_t* tabs, RunIndex* x,
-                       hipStream_t s);
+void launch_run_tables(const RunInfo* runs, uint64_t k, const uint32_t* cf, uint64_t mb, uint64_t n, uint64_t m,
+                       uint32_t* tabs, RunIndex* x, hipStream_t s);
 void launch_new_offsets(const uint64_t* off, uint64_t n, const RunIndex& x, const uint32_t* cf, uint64_t mb, int insert,
                         uint64_t* noff, hipStream_t s);
 void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunIndex& x,
@@ -99,6 +101,10 @@ void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, uint64_
                           int kb, const uint64_t* col_base, uint64_t* skeys, uint32_t* vals, hipStream_t s);
 void launch_index_split(const uint64_t* skeys, uint64_t E, int kb, unsigned long long* counts, uint64_t* keys,
                         hipStream_t s);
+unsigned aff_blocks(uint64_t W);
+void launch_aff_count(const uint8_t* aff, uint64_t W, uint32_t* counts, hipStream_t s);
+void launch_aff_write(const uint8_t* aff, uint64_t W, const uint32_t* offs, uint64_t n, uint64_t n_loc, uint64_t lo,
+                      uint32_t* out, hipStream_t s);
 void launch_li_to_wid(const uint64_t* li, uint64_t cnt, uint64_t n, uint64_t n_loc, uint64_t lo, uint32_t* out,
                       hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s);

@@ -461,23 +461,7 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
 // Blocks for the walk kernels: one walk per lane by default; a smaller grid of
 // lanes each looping over several walks with WHARF_WALK_BLOCKS_PER_CU=k
 // (k blocks of 256 per CU; 0 = one walk per lane).
-static unsigned walk_grid(uint64_t W)
-{
-    static int cus = -1, per_cu = 0;
-    if (cus < 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-        const char* e = getenv("WHARF_WALK_BLOCKS_PER_CU");
-        per_cu = e ? atoi(e) : 0;
-    }
-    const uint64_t full = (W + 255) / 256;
-    if (per_cu <= 0) return (unsigned)full;
-    return (unsigned)std::min<uint64_t>(full, (uint64_t)cus * per_cu);
-}
-
-// resident lanes for the deferred-walk list kernel (8 blocks of 256 per CU)
-static unsigned list_grid()
+unsigned cu_count()
 {
     static int cus = -1;
     if (cus < 0) {
@@ -485,8 +469,23 @@ static unsigned list_grid()
         (void)hipGetDevice(&dev);
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     }
-    return (unsigned)cus * 8;
+    return (unsigned)cus;
 }
+
+static unsigned walk_grid(uint64_t W)
+{
+    static int per_cu = -1;
+    if (per_cu < 0) {
+        const char* e = getenv("WHARF_WALK_BLOCKS_PER_CU");
+        per_cu = e ? std::max(0, atoi(e)) : 0;
+    }
+    const uint64_t full = (W + 255) / 256;
+    if (per_cu <= 0) return (unsigned)full;
+    return (unsigned)std::min<uint64_t>(full, (uint64_t)cu_count() * per_cu);
+}
+
+// resident lanes for the deferred-walk list kernel (8 blocks of 256 per CU)
+static unsigned list_grid() { return cu_count() * 8; }
 
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
 {
@@ -703,12 +702,15 @@ __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* _
     }
 }
 
-// Bucketed index over the source-run table: vtab[b] = first run with
-// src >= b << vs, etab[b] = first run with row offset >= b << es.  A lookup
-// reads one table pair (L2-resident) and binary-searches the few runs of one
-// bucket instead of log2(k) dependent probes over the whole table per edge.
-__global__ void k_run_tables(const RunInfo* __restrict__ runs, uint64_t k, uint32_t* __restrict__ vtab, uint64_t nbv,
-                             uint32_t vs, uint32_t* __restrict__ etab, uint64_t nbe, uint32_t es)
+// Bucketed index over the source-run table: vtab[b] = {first run with
+// src >= b << vs, the row shift of the vertices of bucket b below it},
+// etab[b] = first run with row offset >= b << es.  A lookup reads one table
+// pair (L2-resident) and binary-searches the few runs of one bucket instead of
+// log2(k) dependent probes over the whole table; a vertex in a bucket without
+// a batch source takes its row shift straight from the table.
+__global__ void k_run_tables(const RunInfo* __restrict__ runs, uint64_t k, const uint32_t* __restrict__ cf, uint64_t mb,
+                             uint2* __restrict__ vtab, uint64_t nbv, uint32_t vs, uint32_t* __restrict__ etab,
+                             uint32_t* __restrict__ eshift, uint64_t nbe, uint32_t es)
 {
     const uint64_t nb = nbv > nbe ? nbv : nbe;
     for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
@@ -719,7 +721,7 @@ __global__ void k_run_tables(const RunInfo* __restrict__ runs, uint64_t k, uint3
                 const uint64_t mid = lo + ((hi - lo) >> 1);
                 if (runs[mid].src < t) lo = mid + 1; else hi = mid;
             }
-            vtab[b] = (uint32_t)lo;
+            vtab[b] = make_uint2((uint32_t)lo, cf[lo < k ? runs[lo].rs : mb]);
         }
         if (b < nbe) {
             const uint64_t t = b << es;
@@ -729,6 +731,16 @@ __global__ void k_run_tables(const RunInfo* __restrict__ runs, uint64_t k, uint3
                 if (runs[mid].off < t) lo = mid + 1; else hi = mid;
             }
             etab[b] = (uint32_t)lo;
+            // a clean bucket: no source row starts or runs inside it, so every
+            // slot of it moves by the same shift
+            const uint64_t t2 = (b + 1) << es;
+            uint64_t lo2 = lo, hi2 = k;
+            while (lo2 < hi2) {
+                const uint64_t mid = lo2 + ((hi2 - lo2) >> 1);
+                if (runs[mid].off < t2) lo2 = mid + 1; else hi2 = mid;
+            }
+            const bool clean = lo2 == lo && (lo == 0 || runs[lo - 1].end <= t);
+            eshift[b] = clean ? 0x80000000u | (lo ? cf[runs[lo - 1].re] : 0u) : 0u;
         }
     }
 }
@@ -737,7 +749,7 @@ __global__ void k_run_tables(const RunInfo* __restrict__ runs, uint64_t k, uint3
 __device__ __forceinline__ uint64_t run_lower_src(const RunIndex& x, uint32_t v)
 {
     const uint64_t b = (uint64_t)v >> x.vs;
-    uint64_t lo = x.vtab[b], hi = x.vtab[b + 1];
+    uint64_t lo = x.vtab[b].x, hi = x.vtab[b + 1].x;
     while (lo < hi) {
         const uint64_t mid = lo + ((hi - lo) >> 1);
         if (x.runs[mid].src < v) lo = mid + 1; else hi = mid;
@@ -776,13 +788,23 @@ __global__ void k_new_offsets(const uint64_t* __restrict__ off, uint64_t n, RunI
 __device__ __forceinline__ ERec patch_rec(const ERec r, const RunIndex& x, const uint32_t* __restrict__ cf, uint64_t mb,
                                           int insert, uint32_t epoch)
 {
-    const RunInfo* __restrict__ runs = x.runs;
-    const uint64_t k = x.k;
     const uint32_t v = r.v;
-    const uint64_t lo = run_lower_src(x, v);
-    const uint64_t shift = lo < k ? cf[runs[lo].rs] : cf[mb];
+    const uint64_t b = (uint64_t)v >> x.vs;
+    const uint2 t0 = x.vtab[b], t1 = x.vtab[b + 1];
     uint64_t off = r.oe & kOffMask;
     uint32_t ep = (uint32_t)(r.oe >> kOffBits), deg = r.deg;
+    if (t0.x == t1.x) {   // no batch source in v's bucket (the common case)
+        off = insert ? off + t0.y : off - t0.y;
+        return make_rec(v, deg, off, ep);
+    }
+    const RunInfo* __restrict__ runs = x.runs;
+    const uint64_t k = x.k;
+    uint64_t lo = t0.x, hi = t1.x;
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (runs[mid].src < v) lo = mid + 1; else hi = mid;
+    }
+    const uint64_t shift = lo < k ? cf[runs[lo].rs] : cf[mb];
     off = insert ? off + shift : off - shift;
     if (lo < k && runs[lo].src == v) {
         const uint32_t d = cf[runs[lo].re] - cf[runs[lo].rs];
@@ -792,21 +814,66 @@ __device__ __forceinline__ ERec patch_rec(const ERec r, const RunIndex& x, const
     return make_rec(v, deg, off, ep);
 }
 
-__global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* __restrict__ anc, uint64_t m,
+// LDS = true (up to 10 k source runs, 80 KiB): the source ids and their row shifts sit in
+// LDS, so the target-record patch is a binary search in LDS instead of a
+// random L2 lookup per edge (random lookups, even L2 hits, cap the kernel at
+// the chip's random-access rate, ~45 G/s: 1.9 ms for configs[2]'s 86 M edges).
+template <bool LDS>
+__global__ __launch_bounds__(LDS ? 1024 : 256) void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* __restrict__ anc, uint64_t m,
                              RunIndex rx, const uint64_t* __restrict__ bkeys,
                              const uint32_t* __restrict__ cf, const uint64_t* __restrict__ noff, int insert,
                              uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc, uint64_t cap,
                              const ERec* __restrict__ oerec, ERec* __restrict__ nerec, uint64_t mb, uint32_t epoch)
 {
     const RunInfo* __restrict__ runs = rx.runs;
+    extern __shared__ uint32_t s_tab[];   // LDS: src[k + 1] (sentinel ~0), shift[k + 1]
+    const uint32_t k = (uint32_t)rx.k;
+    if constexpr (LDS) {
+        for (uint32_t j = threadIdx.x; j <= k; j += blockDim.x) {
+            s_tab[j] = j < k ? runs[j].src : ~0u;
+            s_tab[k + 1 + j] = cf[j < k ? runs[j].rs : mb];
+        }
+        __syncthreads();
+    }
+    auto patch = [&](const ERec r) -> ERec {
+        if constexpr (!LDS) {
+            return patch_rec(r, rx, cf, mb, insert, epoch);
+        } else {
+            uint32_t lo = 0, hi = k;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_tab[mid] < r.v) lo = mid + 1; else hi = mid;
+            }
+            const uint64_t shift = s_tab[k + 1 + lo];
+            uint64_t off = r.oe & kOffMask;
+            uint32_t ep = (uint32_t)(r.oe >> kOffBits), deg = r.deg;
+            off = insert ? off + shift : off - shift;
+            if (s_tab[lo] == r.v) {   // a batch source (rare): degree change, sampler reset
+                const uint32_t d = cf[runs[lo].re] - cf[runs[lo].rs];
+                deg = insert ? deg + d : deg - d;
+                ep = epoch;
+            }
+            return make_rec(r.v, deg, off, ep);
+        }
+    };
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t x = adj[e];
+        const uint32_t es = rx.eshift[e >> rx.es];
+        if (es >> 31) {   // clean bucket: shift from the table, no run search
+            const uint64_t shift = es & 0x7FFFFFFFu;
+            const uint64_t np = insert ? e + shift : e - shift;
+            if (np >= cap) continue;
+            nadj[np] = x;
+            if (nanc) nanc[np] = anc[e];
+            if (nerec) nerec[np] = patch(oerec[e]);
+            continue;
+        }
         // last source run whose row starts at or before e
         const uint64_t lo = run_upper_off(rx, e);
-        const uint32_t x = adj[e];
         if (lo == 0) {
             nadj[e] = x;
             if (nanc) nanc[e] = anc[e];
-            if (nerec) nerec[e] = patch_rec(oerec[e], rx, cf, mb, insert, epoch);
+            if (nerec) nerec[e] = patch(oerec[e]);
             continue;
         }
         const RunInfo ri = runs[lo - 1];
@@ -829,7 +896,7 @@ __global__ void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* _
             if (np >= cap) continue;
             nadj[np] = x;
             if (nanc) nanc[np] = anc[e];
-            if (nerec) nerec[np] = patch_rec(oerec[e], rx, cf, mb, insert, epoch);
+            if (nerec) nerec[np] = patch(oerec[e]);
         }
     }
 }
@@ -966,6 +1033,76 @@ __global__ void k_index_split(const uint64_t* __restrict__ skeys, uint64_t E, in
     }
 }
 
+// Affected walk ids, ascending, as a two-pass stream compaction of aff[]
+// (1 B per owned walk, kNoRewalk = unaffected): 16 walks per thread (one
+// 16-B load), 4096 per block.  Pass 1 counts per block; an exclusive scan
+// of the block counts; pass 2 writes each affected walk's id (wid, not the
+// local column) at its rank.
+constexpr uint32_t kAffPerThread = 16, kAffPerBlock = 256 * kAffPerThread;
+
+__device__ __forceinline__ uint32_t aff_count16(const uint8_t* __restrict__ aff, uint64_t W, uint64_t base)
+{
+    uint32_t c = 0;
+    if (base + kAffPerThread <= W) {
+        const uint4 q = *reinterpret_cast<const uint4*>(aff + base);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) c += ((w[k] >> (8 * b)) & 0xFFu) != kNoRewalk;
+    } else {
+        for (uint64_t i = base; i < W; i++) c += aff[i] != kNoRewalk;
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(256) void k_aff_count(const uint8_t* __restrict__ aff, uint64_t W, uint32_t* __restrict__ counts)
+{
+    const uint64_t base = (uint64_t)blockIdx.x * kAffPerBlock + (uint64_t)threadIdx.x * kAffPerThread;
+    uint32_t c = base < W ? aff_count16(aff, W, base) : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    __shared__ uint32_t part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+__global__ __launch_bounds__(256) void k_aff_write(const uint8_t* __restrict__ aff, uint64_t W, const uint32_t* __restrict__ offs,
+                                                   uint64_t n, uint64_t n_loc, uint64_t lo, uint32_t* __restrict__ out)
+{
+    const uint64_t base = (uint64_t)blockIdx.x * kAffPerBlock + (uint64_t)threadIdx.x * kAffPerThread;
+    const uint32_t c = base < W ? aff_count16(aff, W, base) : 0;
+    // block-exclusive prefix of the per-thread counts
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    __shared__ uint32_t part[4];
+    if (lane == 63) part[wv] = x;
+    __syncthreads();
+    uint32_t pre = x - c;
+    for (uint32_t k = 0; k < wv; k++) pre += part[k];
+    uint64_t at = (uint64_t)offs[blockIdx.x] + pre;
+    if (!c) return;
+    const uint64_t end = base + kAffPerThread < W ? base + kAffPerThread : W;
+    for (uint64_t l = base; l < end; l++) {
+        if (aff[l] == kNoRewalk) continue;
+        const uint64_t r = l / n_loc;
+        out[at++] = (uint32_t)(r * n + lo + (l - r * n_loc));
+    }
+}
+
+unsigned aff_blocks(uint64_t W) { return (unsigned)((W + kAffPerBlock - 1) / kAffPerBlock); }
+void launch_aff_count(const uint8_t* aff, uint64_t W, uint32_t* counts, hipStream_t s)
+{ if (W) hipLaunchKernelGGL(k_aff_count, aff_blocks(W), 256, 0, s, aff, W, counts); }
+void launch_aff_write(const uint8_t* aff, uint64_t W, const uint32_t* offs, uint64_t n, uint64_t n_loc, uint64_t lo,
+                      uint32_t* out, hipStream_t s)
+{ if (W) hipLaunchKernelGGL(k_aff_write, aff_blocks(W), 256, 0, s, aff, W, offs, n, n_loc, lo, out); }
+
 __global__ void k_li_to_wid(const uint64_t* __restrict__ li, uint64_t cnt, uint64_t n, uint64_t n_loc, uint64_t lo,
                             uint32_t* __restrict__ out)
 {
@@ -1037,18 +1174,20 @@ void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
                      RunInfo* runs, uint32_t* bitmap, uint32_t* row_epoch, uint32_t epoch, hipStream_t s)
 { hipLaunchKernelGGL(k_run_info, grid_for(k, 256), 256, 0, s, bkeys, run_start, k, mb, off, runs, bitmap, row_epoch, epoch); }
-void launch_run_tables(const RunInfo* runs, uint64_t k, uint64_t n, uint64_t m, uint32_t* tabs, RunIndex* x,
-                       hipStream_t s)
+void launch_run_tables(const RunInfo* runs, uint64_t k, const uint32_t* cf, uint64_t mb, uint64_t n, uint64_t m,
+                       uint32_t* tabs, RunIndex* x, hipStream_t s)
 {
     x->runs = runs;
     x->k = k;
     x->vs = run_table_shift(n, 18);
     x->es = run_table_shift(m, 20);
     const uint64_t nbv = (n >> x->vs) + 2, nbe = (m >> x->es) + 2;
-    x->vtab = tabs;
-    x->etab = tabs + nbv;
-    hipLaunchKernelGGL(k_run_tables, grid_for(std::max(nbv, nbe), 256), 256, 0, s, runs, k, tabs, nbv, x->vs,
-                       tabs + nbv, nbe, x->es);
+    uint2* vt = reinterpret_cast<uint2*>(tabs);
+    x->vtab = vt;
+    x->etab = tabs + 2 * nbv;
+    x->eshift = tabs + 2 * nbv + nbe;
+    hipLaunchKernelGGL(k_run_tables, grid_for(std::max(nbv, nbe), 256), 256, 0, s, runs, k, cf, mb, vt, nbv, x->vs,
+                       tabs + 2 * nbv, tabs + 2 * nbv + nbe, nbe, x->es);
 }
 void launch_new_offsets(const uint64_t* off, uint64_t n, const RunIndex& x, const uint32_t* cf, uint64_t mb, int insert,
                         uint64_t* noff, hipStream_t s)
@@ -1058,9 +1197,24 @@ void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, con
                        uint64_t* nanc, uint64_t cap, const ERec* oerec, ERec* nerec, uint64_t mb, uint32_t epoch,
                        hipStream_t s)
 {
-    if (m)
-        hipLaunchKernelGGL(k_move_edges, grid_for(m, 256), 256, 0, s, adj, anc, m, x, bkeys, cf, noff, insert, nadj,
-                           nanc, cap, oerec, nerec, mb, epoch);
+    if (!m) return;
+    static int max_lds = -1;   // LDS per workgroup (160 KiB on gfx950); two workgroups per CU
+    if (max_lds < 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) max_lds = 65536;
+        max_lds = std::min(max_lds, 80 * 1024);
+    }
+    const char* no_lds = getenv("WHARF_MOVE_NO_LDS");   // tests: force the L2-table path
+    if ((x.k + 1) * 8 <= (uint64_t)max_lds && !(no_lds && *no_lds == '1')) {
+        const size_t lds = (size_t)(x.k + 1) * 8;
+        const unsigned grid = (unsigned)std::min<uint64_t>((m + 1023) / 1024, (uint64_t)cu_count() * 2);
+        hipLaunchKernelGGL(k_move_edges<true>, grid, 1024, lds, s, adj, anc, m, x, bkeys, cf, noff, insert, nadj, nanc,
+                           cap, oerec, nerec, mb, epoch);
+    } else {
+        hipLaunchKernelGGL(k_move_edges<false>, grid_for(m, 256), 256, 0, s, adj, anc, m, x, bkeys, cf, noff, insert,
+                           nadj, nanc, cap, oerec, nerec, mb, epoch);
+    }
 }
 void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf, const uint32_t* run_start,
                       uint64_t k, const RunInfo* runs, const uint32_t* adj, const uint64_t* noff, uint32_t* nadj,
