@@ -91,6 +91,7 @@ struct wharf_handle {
     std::string err;
 
     void sync() { HIPCHK(hipStreamSynchronize(s)); }
+    uint64_t bitmap_words() const { return (n + 31) / 32 + 1; }
 
     template <class F> void rp(F&& f)   // run a rocPRIM call with the shared temp buffer
     {
@@ -144,7 +145,7 @@ struct wharf_handle {
             anchor.ensure(std::max<uint64_t>(m, 1) * 8, true);
             launch_fill_u64(anchor.as<uint64_t>(), m, kAnchorNone64, s);
         }
-        bitmap.ensure(((n + 31) / 32 + 1) * 4);
+        bitmap.ensure((bitmap_words() + kBloomWords) * 4);   // exact bitmap, then the Bloom filter
         sync();
     }
 
@@ -193,6 +194,7 @@ struct wharf_handle {
         a.walks = walks.as<uint32_t>();
         a.rtab = rtab.as<uint64_t>();
         a.bitmap = bitmap.as<uint32_t>();
+        a.bloom = bitmap.as<uint32_t>() + bitmap_words();
         a.aff = aff.as<uint8_t>();
         a.counters = counters.as<unsigned long long>();
         a.n = n; a.n_loc = n_loc; a.lo = lo; a.W = W;
@@ -415,9 +417,10 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         const uint64_t m_new = insert ? h->m + total_chg : h->m - total_chg;
         h->epoch++;
         h->runs.ensure(k * sizeof(RunInfo));
-        HIPCHK(hipMemsetAsync(h->bitmap.p, 0, ((h->n + 31) / 32 + 1) * 4, s));
+        HIPCHK(hipMemsetAsync(h->bitmap.p, 0, (h->bitmap_words() + kBloomWords) * 4, s));
         launch_run_info(bkeys, h->runstart.as<uint32_t>(), k, mb, h->off.as<uint64_t>(), h->runs.as<RunInfo>(),
-                        h->bitmap.as<uint32_t>(), h->row_epoch.as<uint32_t>(), h->epoch, s);
+                        h->bitmap.as<uint32_t>(), h->bitmap.as<uint32_t>() + h->bitmap_words(),
+                        h->row_epoch.as<uint32_t>(), h->epoch, s);
         h->off2.ensure((h->n + 1) * 8);
         h->adj2.ensure(std::max<uint64_t>(m_new, 1) * 4, true);
         if (h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8, true);

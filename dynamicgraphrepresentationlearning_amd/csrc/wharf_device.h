@@ -17,6 +17,9 @@ namespace wharf {
 constexpr uint32_t kSent = 0xFFFFFFFEu;        // wharfmh.h:282 (uint32 max - 1)
 constexpr uint32_t kAnchorNone = 0xFFFFFFFFu;  // MH anchor slot not initialised yet
 constexpr uint32_t kNoRewalk = 0xFFu;          // rewalk position "none"
+constexpr uint32_t kBloomWords = 4096;         // batch-source Bloom filter: 2^17 bits (16 KiB, LDS)
+
+__host__ __device__ __forceinline__ uint32_t bloom_hash(uint32_t x) { return (x * 2654435761u) >> 15; }
 
 // Philox counter word 3 = (epoch << 4) | stream
 enum : uint32_t { kStreamStep = 0, kStreamAnchor = 1, kStreamBurnin = 2, kStreamPrev = 3 };

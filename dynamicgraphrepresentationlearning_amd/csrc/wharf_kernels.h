@@ -24,6 +24,7 @@ struct WalkArgs {
     uint32_t* walks;             // [L][W]
     const uint64_t* rtab;        // deterministic draws [wpv][L]
     const uint32_t* bitmap;      // batch sources (re-walk)
+    const uint32_t* bloom;       // Bloom filter of the batch sources, kBloomWords
     uint8_t* aff;                // per owned walk: re-walk position or kNoRewalk
     unsigned long long* counters;  // [0] steps, [1] accepts
     uint64_t n, n_loc, lo, W;
@@ -78,7 +79,8 @@ void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off
                          uint32_t* chg, hipStream_t s);
 void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_t s);
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
-                     RunInfo* runs, uint32_t* bitmap, uint32_t* row_epoch, uint32_t epoch, hipStream_t s);
+                     RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, uint32_t* row_epoch, uint32_t epoch,
+                     hipStream_t s);
 void launch_run_tables(const RunInfo* runs, uint64_t k, const uint32_t* cf, uint64_t mb, uint64_t n, uint64_t m,
                        uint32_t* tabs, RunIndex* x, hipStream_t s);
 void launch_new_offsets(const uint64_t* off, uint64_t n, const RunIndex& x, const uint32_t* cf, uint64_t mb, int insert,

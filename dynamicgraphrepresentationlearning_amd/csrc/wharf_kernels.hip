@@ -249,9 +249,30 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
 // so the scan of late-starting lanes hides behind the walking of the others.
 enum : uint32_t { kLaneScan = 0, kLaneWalk = 1, kLaneDone = 2 };
 
+// Batch-source test of the rewalk-point scan: a 16-KiB Bloom filter of the
+// batch sources (one hash, 2^17 bits: <= 8 % false positives at 10 k sources)
+// in LDS answers most positions; only its positives read the exact bitmap.
+// Without it every scanned position is a random L2 read of the n-bit bitmap
+// (1.6 G per configs[2] batch, the re-walk kernel's only extra cost over
+// generation).
+__device__ __forceinline__ void bloom_to_lds(const WalkArgs& a, uint32_t* s_bloom)
+{
+    for (uint32_t i = threadIdx.x; i < kBloomWords; i += blockDim.x) s_bloom[i] = a.bloom[i];
+    __syncthreads();
+}
+
+__device__ __forceinline__ bool is_source(const WalkArgs& a, const uint32_t* s_bloom, uint32_t x)
+{
+    const uint32_t h = bloom_hash(x);
+    if (!((s_bloom[h >> 5] >> (h & 31)) & 1u)) return false;
+    return (a.bitmap[x >> 5] >> (x & 31)) & 1u;
+}
+
 template <int MODEL, bool DET>
 __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
 {
+    __shared__ uint32_t s_bloom[kBloomWords];
+    bloom_to_lds(a, s_bloom);
     uint32_t steps = 0, accepts = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t* __restrict__ walks = a.walks;
@@ -291,7 +312,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
                 val = x;
                 if (x == kSent) {
                     mode = kLaneDone;   // old walk ended: no batch source on it
-                } else if ((a.bitmap[x >> 5] >> (x & 31)) & 1u) {
+                } else if (is_source(a, s_bloom, x)) {
                     p = pos;
                     mode = a.scan_only ? kLaneDone : kLaneWalk;
                     if (!a.scan_only) walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, rc, rp, ein);
@@ -328,6 +349,8 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
 template <int MODEL, bool DET>
 __global__ __launch_bounds__(256) void k_rewalk(WalkArgs a)
 {
+    __shared__ uint32_t s_bloom[kBloomWords];
+    bloom_to_lds(a, s_bloom);
     uint32_t steps = 0, accepts = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t* __restrict__ walks = a.walks;
@@ -349,7 +372,7 @@ __global__ __launch_bounds__(256) void k_rewalk(WalkArgs a)
                 if (x == kSent) break;
                 if (pos + 1 < L) xn = walks[(uint64_t)(pos + 1) * W + li];
             }
-            if ((a.bitmap[x >> 5] >> (x & 31)) & 1u) { p = pos; break; }
+            if (is_source(a, s_bloom, x)) { p = pos; break; }
         }
         a.aff[li] = (uint8_t)p;
         if (a.scan_only) continue;
@@ -490,7 +513,10 @@ static unsigned list_grid() { return cu_count() * 8; }
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
 {
     if (a.W == 0) return;
-    const dim3 grid(walk_grid(a.W)), block(256);
+    // re-walks: persistent blocks (8 per CU, 16 KiB of Bloom filter each), so
+    // the filter is copied to LDS once per block, not once per 256 walks
+    const dim3 grid(rewalk ? std::min<uint64_t>((a.W + 255) / 256, (uint64_t)cu_count() * 8) : walk_grid(a.W)),
+        block(256);
     const dim3 lgrid(list_grid());
 #define WHARF_LAUNCH(M, D)                                                                   \
     do {                                                                                     \
@@ -688,7 +714,8 @@ __global__ void k_run_flags(const uint64_t* __restrict__ bkeys, uint64_t mb, uin
 // per source run j: src, old row [off, end), batch run [rs, re)
 __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ run_start, uint64_t k,
                            uint64_t mb, const uint64_t* __restrict__ off, RunInfo* __restrict__ runs,
-                           uint32_t* __restrict__ bitmap, uint32_t* __restrict__ row_epoch, uint32_t epoch)
+                           uint32_t* __restrict__ bitmap, uint32_t* __restrict__ bloom, uint32_t* __restrict__ row_epoch,
+                           uint32_t epoch)
 {
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t rs = run_start[j];
@@ -698,6 +725,8 @@ __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* _
         ri.src = s; ri.rs = rs; ri.re = re; ri.off = off[s]; ri.end = off[s + 1];
         runs[j] = ri;
         atomicOr(bitmap + (s >> 5), 1u << (s & 31));
+        const uint32_t h = bloom_hash(s);
+        atomicOr(bloom + (h >> 5), 1u << (h & 31));
         if (row_epoch) row_epoch[s] = epoch;   // the source's samplers are reset (wharfmh.h:504,539)
     }
 }
@@ -1172,8 +1201,9 @@ void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off
 void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_t s)
 { hipLaunchKernelGGL(k_run_flags, grid_for(mb, 256), 256, 0, s, bkeys, mb, f); }
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
-                     RunInfo* runs, uint32_t* bitmap, uint32_t* row_epoch, uint32_t epoch, hipStream_t s)
-{ hipLaunchKernelGGL(k_run_info, grid_for(k, 256), 256, 0, s, bkeys, run_start, k, mb, off, runs, bitmap, row_epoch, epoch); }
+                     RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, uint32_t* row_epoch, uint32_t epoch,
+                     hipStream_t s)
+{ hipLaunchKernelGGL(k_run_info, grid_for(k, 256), 256, 0, s, bkeys, run_start, k, mb, off, runs, bitmap, bloom, row_epoch, epoch); }
 void launch_run_tables(const RunInfo* runs, uint64_t k, const uint32_t* cf, uint64_t mb, uint64_t n, uint64_t m,
                        uint32_t* tabs, RunIndex* x, hipStream_t s)
 {
