@@ -83,7 +83,7 @@ struct wharf_handle {
     uint32_t L = 0, wpv = 0;
     bool anchors = false, has_walks = false;
     uint32_t epoch = 0;
-    DevBuf off, adj, vrec, erec, anchor, row_epoch, off2, adj2, anchor2, ehash, erec2;
+    DevBuf off, adj, vrec, erec, row_epoch, off2, adj2, anchor2, ehash, erec2;
     uint64_t ehash_mask = 0, ehash_used = 0;   // capacity - 1; occupied slots incl. tombstones
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
     DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, rtabs, count, pairs, sel, defer;
@@ -141,10 +141,7 @@ struct wharf_handle {
         row_epoch.ensure(std::max<uint64_t>(n, 1) * 4);
         HIPCHK(hipMemsetAsync(row_epoch.p, 0, std::max<uint64_t>(n, 1) * 4, s));
         build_records();
-        if (anchors) {
-            anchor.ensure(std::max<uint64_t>(m, 1) * 8, true);
-            launch_fill_u64(anchor.as<uint64_t>(), m, kAnchorNone64, s);
-        }
+        if (anchors) build_edge_hash();
         bitmap.ensure((bitmap_words() + kBloomWords) * 4);   // exact bitmap, then the Bloom filter
         sync();
     }
@@ -159,15 +156,17 @@ struct wharf_handle {
         has_walks = false;
     }
 
-    // vertex rows and per-slot edge records (one 16-B gather per walk step);
-    // node2vec MH also gets the edge hash set for has_edge
+    // 16-B edge records, 32 B with the anchor entry (node2vec MH)
+    uint64_t rec_stride() const { return anchors ? 2 : 1; }
+
+    // vertex rows and per-slot edge records (one gather per walk step);
+    // anchor entries start empty
     void build_records()
     {
         vrec.ensure(std::max<uint64_t>(n, 1) * sizeof(ERec));
-        erec.ensure(std::max<uint64_t>(m, 1) * sizeof(ERec), true);
+        erec.ensure(std::max<uint64_t>(m, 1) * sizeof(ERec) * rec_stride(), true);
         launch_vrec(off.as<uint64_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
-        launch_erec(adj.as<uint32_t>(), m, vrec.as<ERec>(), erec.as<ERec>(), s);
-        if (anchors) build_edge_hash();
+        launch_erec(adj.as<uint32_t>(), m, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rec_stride(), s);
     }
 
     void build_edge_hash()
@@ -188,7 +187,7 @@ struct wharf_handle {
         a.vrec = vrec.as<ERec>();
         a.erec = erec.as<ERec>();
         a.adj = adj.as<uint32_t>();
-        a.anchor = anchors ? anchor.as<uint64_t>() : nullptr;
+        a.anchor = anchors ? erec.as<uint64_t>() + 2 : nullptr;   // inside the 32-B records
         a.ehash = anchors ? ehash.as<uint64_t>() : nullptr;
         a.ehash_mask = ehash_mask;
         a.walks = walks.as<uint32_t>();
@@ -303,7 +302,7 @@ void free_handle(wharf_handle* h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->s) (void)hipStreamSynchronize(h->s);
-    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->anchor, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
+    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
                       &h->aff, &h->rtab, &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags,
                       &h->chg, &h->cf, &h->runstart, &h->runs, &h->rtabs, &h->count, &h->pairs, &h->sel, &h->defer})
         b->release();
@@ -423,51 +422,60 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
                         h->row_epoch.as<uint32_t>(), h->epoch, s);
         h->off2.ensure((h->n + 1) * 8);
         h->adj2.ensure(std::max<uint64_t>(m_new, 1) * 4, true);
-        if (h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8, true);
         RunIndex rx;
         h->rtabs.ensure(run_tables_words(h->n, h->m) * 4);
         launch_run_tables(h->runs.as<RunInfo>(), k, h->cf.as<uint32_t>(), mb, h->n, h->m, h->rtabs.as<uint32_t>(), &rx, s);
         launch_new_offsets(h->off.as<uint64_t>(), h->n, rx, h->cf.as<uint32_t>(), mb, insert, h->off2.as<uint64_t>(), s);
-        // edge records move with their slot and are patched arithmetically when
-        // a second record buffer fits; otherwise they are rebuilt by a gather
-        bool patch = true;
-        try {
-            h->erec2.ensure(std::max<uint64_t>(m_new, 1) * sizeof(ERec), true);
-        } catch (const WharfError&) {
-            (void)hipGetLastError();
-            patch = false;
+        // edge records (node2vec MH: with their anchor entries) move with their
+        // slot and are patched arithmetically when a second record buffer fits;
+        // otherwise they are rebuilt by a gather and the anchors travel through
+        // a separate 8-B-per-slot buffer
+        const uint64_t rs = h->rec_stride();
+        const char* force = getenv("WHARF_FORCE_RECORD_REBUILD");   // tests: the no-room path
+        bool patch = !(force && *force == '1');
+        if (patch) {
+            try {
+                h->erec2.ensure(std::max<uint64_t>(m_new, 1) * sizeof(ERec) * rs, true);
+            } catch (const WharfError&) {
+                (void)hipGetLastError();
+                patch = false;
+            }
         }
-        launch_move_edges(h->adj.as<uint32_t>(), h->anchors ? h->anchor.as<uint64_t>() : nullptr, h->m,
-                          rx, bkeys, h->cf.as<uint32_t>(), h->off2.as<uint64_t>(), insert,
-                          h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint64_t>() : nullptr, m_new,
-                          patch ? h->erec.as<ERec>() : nullptr, patch ? h->erec2.as<ERec>() : nullptr, mb, h->epoch, s);
-        if (insert)
+        if (!patch && h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8, true);
+        uint64_t* anc_in = h->anchors ? h->erec.as<uint64_t>() + 2 : nullptr;
+        uint64_t* anc_out = !h->anchors ? nullptr : patch ? h->erec2.as<uint64_t>() + 2 : h->anchor2.as<uint64_t>();
+        const uint32_t as_out = patch ? (uint32_t)kAnchorStride : 1u;
+        launch_move_edges(h->adj.as<uint32_t>(), anc_in, kAnchorStride, h->m, rx, bkeys, h->cf.as<uint32_t>(),
+                          h->off2.as<uint64_t>(), insert, h->adj2.as<uint32_t>(), anc_out, as_out, m_new,
+                          patch ? h->erec.as<ERec>() : nullptr, patch ? h->erec2.as<ERec>() : nullptr, (uint32_t)rs, mb,
+                          h->epoch, s);
+        if (insert)   // (the records of source rows, new slots included, are rebuilt below)
             launch_place_new(bkeys, mb, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(), h->runstart.as<uint32_t>(), k,
                              h->runs.as<RunInfo>(), h->adj.as<uint32_t>(), h->off2.as<uint64_t>(),
-                             h->adj2.as<uint32_t>(), h->anchors ? h->anchor2.as<uint64_t>() : nullptr, m_new, s);
+                             h->adj2.as<uint32_t>(), patch ? nullptr : anc_out, 1u, m_new, s);
         std::swap(h->off, h->off2);
         std::swap(h->adj, h->adj2);
-        if (h->anchors) std::swap(h->anchor, h->anchor2);
         h->m = m_new;
         if (patch) {
             std::swap(h->erec, h->erec2);
             launch_vrec(h->off.as<uint64_t>(), h->n, h->row_epoch.as<uint32_t>(), h->vrec.as<ERec>(), s);
             launch_erec_rows(h->runs.as<RunInfo>(), k, h->off.as<uint64_t>(), h->adj.as<uint32_t>(),
-                             h->vrec.as<ERec>(), h->erec.as<ERec>(), s);
-            if (h->anchors) {
-                // the edge set changes by the batch's changing edges only; rebuild when
-                // inserts (and tombstones) push the load past 0.6
-                if (insert && (h->ehash_used + total_chg) * 10 > (h->ehash_mask + 1) * 6) {
-                    h->build_edge_hash();
-                } else {
-                    launch_edge_hash_update(bkeys, mb, h->chg.as<uint32_t>(), insert, h->ehash.as<uint64_t>(),
-                                            h->ehash_mask, s);
-                    if (insert) h->ehash_used += total_chg;
-                }
-            }
+                             h->vrec.as<ERec>(), h->erec.as<ERec>(), (uint32_t)rs, s);
         } else {
             h->erec2.release();
             h->build_records();
+            if (h->anchors) launch_anchor_merge(h->anchor2.as<uint64_t>(), h->m, h->erec.as<uint64_t>() + 2, s);
+        }
+        if (h->anchors) {
+            // the edge set changes by the batch's changing edges only; rebuild when
+            // inserts (and tombstones) push the load past 0.6
+            if (insert && (h->ehash_used + total_chg) * 10 > (h->ehash_mask + 1) * 6) {
+                h->build_edge_hash();
+            } else {
+                launch_edge_hash_update(bkeys, mb, h->chg.as<uint32_t>(), insert, h->ehash.as<uint64_t>(),
+                                        h->ehash_mask, s);
+                if (insert) h->ehash_used += total_chg;
+            }
         }
         HIPCHK(hipEventRecord(h->ev[1], s));
 
@@ -936,7 +944,9 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     r.csr_bytes = h->off.cap + h->adj.cap;
     r.records_bytes = h->vrec.cap + h->erec.cap;
     r.walks_bytes = h->walks.cap + h->aff.cap;
-    r.samplers_bytes = h->anchor.cap + h->row_epoch.cap;
+    const uint64_t anchor_part = h->anchors ? h->erec.cap / 2 : 0;   // bytes 16-31 of the 32-B records
+    r.records_bytes -= anchor_part;
+    r.samplers_bytes = anchor_part + h->row_epoch.cap;
     r.edge_hash_bytes = h->ehash.cap;
     r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->anchor2.cap + h->erec2.cap;
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
@@ -956,7 +966,7 @@ int wharf_get_stats(const wharf_handle* h, wharf_stats* out)
     out->m = h->m;
     out->walks = h->W;
     out->hbm_bytes_walks = h->W * h->L * 4;
-    out->hbm_bytes_graph = (h->n + 1) * 8 + h->m * 4 + (h->n + h->m) * sizeof(ERec) + (h->anchors ? h->m * 8 : 0);
+    out->hbm_bytes_graph = (h->n + 1) * 8 + h->m * 4 + (h->n + h->m * h->rec_stride()) * sizeof(ERec);
     return WHARF_OK;
 }
 

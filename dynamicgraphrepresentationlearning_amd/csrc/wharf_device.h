@@ -39,6 +39,7 @@ struct Row {          // unpacked, in registers
 constexpr uint64_t kOffBits = 40;
 constexpr uint64_t kOffMask = (1ull << kOffBits) - 1;
 constexpr uint64_t kAnchorNone64 = ~0ull;
+constexpr uint64_t kAnchorStride = 4;         // u64 words between anchor entries (32-B node2vec edge records)
 constexpr uint64_t kEmptyKey = ~0ull;         // empty slot of the edge hash set
 constexpr uint64_t kTombKey = ~0ull - 1;      // deleted edge (probing continues past it)
 

@@ -18,7 +18,8 @@ struct WalkArgs {
     const ERec* vrec;            // [n]: the row of each vertex
     const ERec* erec;            // [m]: per CSR slot, the target's row
     const uint32_t* adj;         // [m]: CSR targets (binary searches, anchor proposals)
-    uint64_t* anchor;            // node2vec MH: per CSR slot (edge prev->cur) {anchor slot, epoch tag, class}
+    uint64_t* anchor;            // node2vec MH: anchor entry of CSR slot e at anchor[e * kAnchorStride]
+                                 //   (bytes 16-23 of the slot's 32-B edge record)
     const uint64_t* ehash;       // node2vec: edge hash set (u << 32 | v), or null -> binary search
     uint64_t ehash_mask;         // capacity - 1 (power of two)
     uint32_t* walks;             // [L][W]
@@ -68,7 +69,8 @@ unsigned cu_count();
 
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s);
 void launch_vrec(const uint64_t* off, uint64_t n, const uint32_t* row_epoch, ERec* vrec, hipStream_t s);
-void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, hipStream_t s);
+void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s);
+void launch_anchor_merge(const uint64_t* src, uint64_t m, uint64_t* dst, hipStream_t s);
 void launch_rmat_keys(const RmatParams& p, uint64_t M, int directed, uint64_t* keys, hipStream_t s);
 void launch_pairs_to_keys(const uint32_t* pairs, uint64_t m, uint64_t n, uint64_t* keys, unsigned long long* err, hipStream_t s);
 void launch_csr_to_keys(const uint64_t* off, uint64_t n, const uint32_t* tgt, uint64_t* keys, unsigned long long* err, hipStream_t s);
@@ -85,15 +87,15 @@ void launch_run_tables(const RunInfo* runs, uint64_t k, const uint32_t* cf, uint
                        uint32_t* tabs, RunIndex* x, hipStream_t s);
 void launch_new_offsets(const uint64_t* off, uint64_t n, const RunIndex& x, const uint32_t* cf, uint64_t mb, int insert,
                         uint64_t* noff, hipStream_t s);
-void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunIndex& x,
+void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint32_t as_in, uint64_t m, const RunIndex& x,
                        const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
-                       uint64_t* nanc, uint64_t cap, const ERec* oerec, ERec* nerec, uint64_t mb, uint32_t epoch,
-                       hipStream_t s);
+                       uint64_t* nanc, uint32_t as_out, uint64_t cap, const ERec* oerec, ERec* nerec, uint32_t rs,
+                       uint64_t mb, uint32_t epoch, hipStream_t s);
 void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* nadj, const ERec* vrec,
-                      ERec* erec, hipStream_t s);
+                      ERec* erec, uint32_t rs, hipStream_t s);
 void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf,
                       const uint32_t* run_start, uint64_t k, const RunInfo* runs, const uint32_t* adj,
-                      const uint64_t* noff, uint32_t* nadj, uint64_t* nanc, uint64_t cap, hipStream_t s);
+                      const uint64_t* noff, uint32_t* nadj, uint64_t* nanc, uint32_t as_out, uint64_t cap, hipStream_t s);
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s);
 void launch_gather_walk(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* out, hipStream_t s);
 void launch_gather_rows(const uint32_t* walks, uint64_t W, uint32_t L, const uint64_t* list, uint64_t base,

@@ -122,82 +122,118 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp)
 // The entry also keeps the anchor's weight class (it depends only on (prev,
 // anchor) and prev's row, which the tag covers), so an accepted step needs one
 // has_edge, not two.  Entry = slot | tag << 32 | class << 62.
+//
+// node2vec MH keeps the entry of slot e inside e's 32-B edge record (bytes
+// 16-23), so the gather that crosses an edge also brings the anchor of the
+// state it enters: `anc` is that entry, carried by the walker.
 __device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, int64_t ein,
-                                               uint32_t& cls)
+                                               uint64_t anc, uint32_t& cls)
 {
     if (ein >= 0) {
-        const uint64_t e = a.anchor[ein];
-        const uint32_t tag = (uint32_t)(e >> 32) & 0x3FFFFFFFu;
-        if (e != kAnchorNone64 && tag >= rc.epoch && tag >= rp.epoch) {
-            cls = (uint32_t)(e >> 62);
-            return (uint32_t)e;
+        const uint32_t tag = (uint32_t)(anc >> 32) & 0x3FFFFFFFu;
+        if (anc != kAnchorNone64 && tag >= rc.epoch && tag >= rp.epoch) {
+            cls = (uint32_t)(anc >> 62);
+            return (uint32_t)anc;
         }
     }
     const uint32_t an = anchor_init(a, rc, rp);
     cls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + an]);
-    if (ein >= 0) a.anchor[ein] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+    if (ein >= 0) a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     return an;
 }
 
 // ---------------------------------------------------------------------------
 // The walk kernels.  One lane per walk; lane li owns walk matrix column li.
 // The walker carries the record of its current vertex, so a step is ONE
-// dependent 16-B gather: erec[cur.off + pick] = {next vertex, its degree, row
-// offset, row epoch}.
+// dependent gather: erec[cur.off + pick] = {next vertex, its degree, row
+// offset, row epoch} (+ for node2vec MH the anchor entry of the edge).
 // ---------------------------------------------------------------------------
+
+// edge records per slot: 16 B, or 32 B with the anchor entry (node2vec MH)
+template <int MODEL, bool DET>
+constexpr uint64_t kRecStride = (MODEL == kNode2Vec && !DET) ? 2 : 1;
+
+struct Walker {
+    Row rc, rp;      // rows of the current and previous vertex
+    int64_t ein;     // node2vec MH: slot of the edge prev -> cur, or -1
+    uint64_t anc;    // node2vec MH: anchor entry of that slot
+};
+
+template <int MODEL, bool DET>
+__device__ __forceinline__ Row load_edge(const WalkArgs& a, uint64_t e, uint64_t& anc)
+{
+    const Row r = load_rec(a.erec, e * kRecStride<MODEL, DET>);
+    if constexpr (kRecStride<MODEL, DET> == 2) anc = a.anchor[e * kAnchorStride];   // same 32-B record
+    return r;
+}
 
 // One transition cur -> next from position `pos` (deepwalk.h:64-87 /
 // node2vec.h:52-72 through MetropolisHastingsSampler::sample, or the
 // deterministic adj(cur)[Random(wid/n).lrand() % deg] of wharfmh.h:296-304).
+// Advances the walker; returns the new vertex.
 template <int MODEL, bool DET>
-__device__ __forceinline__ Row walk_step(const WalkArgs& a, const Row& rc, const Row& rp, int64_t& ein,
-                                         const uint64_t* __restrict__ rt, uint32_t pos, uint32_t wlo,
-                                         uint32_t whi, uint32_t ep, uint32_t& accepts)
+__device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, const uint64_t* __restrict__ rt,
+                                              uint32_t pos, uint32_t wlo, uint32_t whi, uint32_t ep, uint32_t& accepts)
 {
+    Row nx;
     if constexpr (DET) {
         // rt = Random(wid / n) restarted at the walk's first re-walked position
-        return load_rec(a.erec, rc.off + umod64_32(rt[pos], rc.deg));
+        nx = load_rec(a.erec, w.rc.off + umod64_32(rt[pos], w.rc.deg));
     } else {
         const P4 q = philox4x32_10(wlo, whi, pos, ep | kStreamStep, a.key0, a.key1);
-        const uint32_t ci = (uint32_t)pick32(q.x0, rc.deg);
-        const Row cand = load_rec(a.erec, rc.off + ci);
+        const uint32_t ci = (uint32_t)pick32(q.x0, w.rc.deg);
+        uint64_t canc = kAnchorNone64;
+        const Row cand = load_edge<MODEL, DET>(a, w.rc.off + ci, canc);
         if constexpr (MODEL == kDeepWalk) {
             accepts++;   // weights are all 1: sample() always accepts
-            return cand;
+            nx = cand;
         } else {
             uint32_t acls;
-            const uint32_t ai = anchor_get(a, rc, rp, ein, acls);
+            const uint32_t ai = anchor_get(a, w.rc, w.rp, w.ein, w.anc, acls);
             bool ok = true;   // proposing the anchor itself is always accepted
             if (ai != ci) {
-                const float wc = weight<MODEL>(a, rp, cand.v);
+                const float wc = weight<MODEL>(a, w.rp, cand.v);
                 const float wa = class_weight(a, acls);
                 ok = (wa < wc) || (u01(q.x1, q.x2) <= (double)wc / (double)wa);
             }
             accepts += ok;
-            ein = (int64_t)(rc.off + (ok ? ci : ai));
-            return ok ? cand : load_rec(a.erec, rc.off + ai);
+            w.ein = (int64_t)(w.rc.off + (ok ? ci : ai));
+            if (ok) {
+                nx = cand;
+                w.anc = canc;
+            } else {
+                nx = load_edge<MODEL, DET>(a, w.rc.off + ai, w.anc);
+            }
         }
     }
+    w.rp = w.rc;
+    w.rc = nx;
+    return nx.v;
 }
 
 // Walker state at position p of walk wid (cur = its vertex): the rows of cur
 // and prev and, for node2vec MH, the slot of the edge prev -> cur.
 template <int MODEL, bool DET>
 __device__ __forceinline__ void walk_state(const WalkArgs& a, uint32_t cur, uint32_t prev, uint32_t p, uint32_t wlo,
-                                           uint32_t whi, uint32_t ep, Row& rc, Row& rp, int64_t& ein)
+                                           uint32_t whi, uint32_t ep, Walker& w)
 {
-    rc = load_rec(a.vrec, cur);
-    rp = rc;
-    ein = -1;
+    w.rc = load_rec(a.vrec, cur);
+    w.rp = w.rc;
+    w.ein = -1;
+    w.anc = kAnchorNone64;
     if constexpr (MODEL == kNode2Vec && !DET) {
         if (p > 0) {
-            rp = load_rec(a.vrec, prev);
-        } else if (rc.deg) {
+            w.rp = load_rec(a.vrec, prev);
+        } else if (w.rc.deg) {
             // Node2Vec::initial_state: prev = random neighbour (node2vec.h:42-50)
             const P4 q = philox4x32_10(wlo, whi, 0, ep | kStreamPrev, a.key0, a.key1);
-            rp = load_rec(a.erec, rc.off + pick32(q.x0, rc.deg));
+            uint64_t unused;
+            w.rp = load_edge<MODEL, DET>(a, w.rc.off + pick32(q.x0, w.rc.deg), unused);
         }
-        if (rc.deg) ein = row_find(a.adj, rp, rc.v);
+        if (w.rc.deg) {
+            w.ein = row_find(a.adj, w.rp, w.rc.v);
+            if (w.ein >= 0) w.anc = a.anchor[(uint64_t)w.ein * kAnchorStride];
+        }
     }
 }
 
@@ -217,17 +253,13 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
         const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
         const uint64_t* __restrict__ rt = DET ? a.rtab + r * a.L : nullptr;
         walks[li] = v;
-        Row rc, rp;
-        int64_t ein;
-        walk_state<MODEL, DET>(a, v, v, 0, wlo, whi, ep, rc, rp, ein);
+        Walker w;
+        walk_state<MODEL, DET>(a, v, v, 0, wlo, whi, ep, w);
         uint32_t pos = 0;
         for (; pos + 1 < a.L; pos++) {
-            if (rc.deg == 0) break;   // dead end: the walk stops (reference: lrand() % 0)
-            const Row nx = walk_step<MODEL, DET>(a, rc, rp, ein, rt, pos, wlo, whi, ep, accepts);
-            walks[(uint64_t)(pos + 1) * W + li] = nx.v;
+            if (w.rc.deg == 0) break;   // dead end: the walk stops (reference: lrand() % 0)
+            walks[(uint64_t)(pos + 1) * W + li] = walk_step<MODEL, DET>(a, w, rt, pos, wlo, whi, ep, accepts);
             steps++;
-            rp = rc;
-            rc = nx;
         }
         for (pos = pos + 1; pos < a.L; pos++) walks[(uint64_t)pos * W + li] = kSent;
     }
@@ -287,20 +319,15 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
         uint32_t mode = kLaneScan, p = kNoRewalk;
         uint32_t x = v, xprev = v;                       // old value at pos, at pos - 1
         uint32_t xn = L > 1 ? walks[W + li] : kSent;     // old value at pos + 1 (prefetched)
-        Row rc, rp;
-        rc.deg = 0;
-        int64_t ein = -1;
+        Walker w;
+        w.rc.deg = 0;
         for (uint32_t pos = 0; pos < L; pos++) {
             uint32_t val = kSent;
             bool fresh = false;
             if (mode == kLaneWalk) {
-                if (rc.deg) {
-                    const Row nx = walk_step<MODEL, DET>(a, rc, rp, ein, rt, DET ? pos - 1 - p : pos - 1, wlo, whi,
-                                                         ep, accepts);
-                    val = nx.v;
+                if (w.rc.deg) {
+                    val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts);
                     steps++;
-                    rp = rc;
-                    rc = nx;
                 }
                 fresh = true;
             } else if (mode == kLaneScan) {
@@ -315,7 +342,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
                 } else if (is_source(a, s_bloom, x)) {
                     p = pos;
                     mode = a.scan_only ? kLaneDone : kLaneWalk;
-                    if (!a.scan_only) walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, rc, rp, ein);
+                    if (!a.scan_only) walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, w);
                 }
             }
             if (!a.scan_only && __any(fresh)) {
@@ -393,10 +420,9 @@ __global__ __launch_bounds__(256) void k_rewalk(WalkArgs a)
             }
         }
         // B. walker state at the rewalk point
-        Row rc, rp;
-        rc.deg = 0;
-        int64_t ein = -1;
-        if (active) walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, rc, rp, ein);
+        Walker w;
+        w.rc.deg = 0;
+        if (active) walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, w);
         // C. lock-step sweep from the wave's smallest rewalk point
         uint32_t first = active ? p + 1 : L;
 #pragma unroll
@@ -406,13 +432,9 @@ __global__ __launch_bounds__(256) void k_rewalk(WalkArgs a)
             uint32_t val;
             if (active && pos > p) {
                 val = kSent;
-                if (rc.deg) {
-                    const Row nx = walk_step<MODEL, DET>(a, rc, rp, ein, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep,
-                                                         accepts);
-                    val = nx.v;
+                if (w.rc.deg) {
+                    val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts);
                     steps++;
-                    rp = rc;
-                    rc = nx;
                 }
             } else {
                 val = walks[at];   // not (yet) re-walking: keep the old value
@@ -443,9 +465,8 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
     uint64_t li = 0;
     uint32_t p = 0, pos = L, wlo = 0, whi = 0;
     const uint64_t* __restrict__ rt = nullptr;
-    Row rc, rp;
-    rc.deg = 0;
-    int64_t ein = -1;
+    Walker w;
+    w.rc.deg = 0;
     for (;;) {
         if (pos >= L && i < cnt) {   // next walk of this lane
             const uint64_t e = a.defer[i];
@@ -459,19 +480,15 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
             if constexpr (DET) rt = a.rtab + r * L;
             const uint32_t x = walks[(uint64_t)p * W + li];
             const uint32_t xprev = p ? walks[(uint64_t)(p - 1) * W + li] : x;
-            walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, rc, rp, ein);
+            walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, w);
             pos = p + 1;
         }
         if (!__any(pos < L)) break;
         if (pos < L) {
             uint32_t val = kSent;
-            if (rc.deg) {
-                const Row nx = walk_step<MODEL, DET>(a, rc, rp, ein, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep,
-                                                     accepts);
-                val = nx.v;
+            if (w.rc.deg) {
+                val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts);
                 steps++;
-                rp = rc;
-                rc = nx;
             }
             walks[(uint64_t)pos * W + li] = val;
             pos++;
@@ -668,11 +685,15 @@ __global__ void k_vrec(const uint64_t* __restrict__ off, uint64_t n, const uint3
         vrec[v] = make_rec((uint32_t)v, (uint32_t)(off[v + 1] - off[v]), off[v], row_epoch ? row_epoch[v] : 0u);
 }
 
-// erec[e] = vrec[adj[e]]: every CSR slot carries its target's row
-__global__ void k_erec(const uint32_t* __restrict__ adj, uint64_t m, const ERec* __restrict__ vrec, ERec* __restrict__ erec)
+// erec[e] = vrec[adj[e]]: every CSR slot carries its target's row (rs = 2:
+// 32-B records whose anchor entry starts empty)
+__global__ void k_erec(const uint32_t* __restrict__ adj, uint64_t m, const ERec* __restrict__ vrec, ERec* __restrict__ erec,
+                       uint32_t rs)
 {
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x)
-        erec[e] = vrec[adj[e]];
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
+        erec[e * rs] = vrec[adj[e]];
+        if (rs == 2) reinterpret_cast<uint64_t*>(erec)[e * kAnchorStride + 2] = kAnchorNone64;
+    }
 }
 
 void launch_vrec(const uint64_t* off, uint64_t n, const uint32_t* row_epoch, ERec* vrec, hipStream_t s)
@@ -680,9 +701,21 @@ void launch_vrec(const uint64_t* off, uint64_t n, const uint32_t* row_epoch, ERe
     if (n) hipLaunchKernelGGL(k_vrec, grid_for(n, 256), 256, 0, s, off, n, row_epoch, vrec);
 }
 
-void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, hipStream_t s)
+void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s)
 {
-    if (m) hipLaunchKernelGGL(k_erec, grid_for(m, 256), 256, 0, s, adj, m, vrec, erec);
+    if (m) hipLaunchKernelGGL(k_erec, grid_for(m, 256), 256, 0, s, adj, m, vrec, erec, rs);
+}
+
+// anchors kept aside by an update without a second record buffer -> records
+__global__ void k_anchor_merge(const uint64_t* __restrict__ src, uint64_t m, uint64_t* __restrict__ dst)
+{
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x)
+        dst[e * kAnchorStride] = src[e];
+}
+
+void launch_anchor_merge(const uint64_t* src, uint64_t m, uint64_t* dst, hipStream_t s)
+{
+    if (m) hipLaunchKernelGGL(k_anchor_merge, grid_for(m, 256), 256, 0, s, src, m, dst);
 }
 
 // Per batch edge (sorted, unique): does it change its source row?
@@ -843,16 +876,21 @@ __device__ __forceinline__ ERec patch_rec(const ERec r, const RunIndex& x, const
     return make_rec(v, deg, off, ep);
 }
 
-// LDS = true (up to 10 k source runs, 80 KiB): the source ids and their row shifts sit in
-// LDS, so the target-record patch is a binary search in LDS instead of a
-// random L2 lookup per edge (random lookups, even L2 hits, cap the kernel at
-// the chip's random-access rate, ~45 G/s: 1.9 ms for configs[2]'s 86 M edges).
+// LDS = true (up to 10 k source runs, 80 KiB): the source ids and their row
+// shifts sit in LDS, so the target-record patch is a binary search in LDS
+// instead of a random L2 lookup per edge (random lookups, even L2 hits, cap
+// the kernel at the chip's random-access rate, ~45 G/s: 1.9 ms for
+// configs[2]'s 86 M edges).
+// Records have stride rs (1: 16 B, 2: 32 B with the anchor entry); anchors
+// are read with stride as_in and written with stride as_out (inside the
+// records, or to a plain array when the records are rebuilt afterwards).
 template <bool LDS>
-__global__ __launch_bounds__(LDS ? 1024 : 256) void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* __restrict__ anc, uint64_t m,
-                             RunIndex rx, const uint64_t* __restrict__ bkeys,
+__global__ __launch_bounds__(LDS ? 1024 : 256) void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* __restrict__ anc,
+                             uint32_t as_in, uint64_t m, RunIndex rx, const uint64_t* __restrict__ bkeys,
                              const uint32_t* __restrict__ cf, const uint64_t* __restrict__ noff, int insert,
-                             uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc, uint64_t cap,
-                             const ERec* __restrict__ oerec, ERec* __restrict__ nerec, uint64_t mb, uint32_t epoch)
+                             uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc, uint32_t as_out, uint64_t cap,
+                             const ERec* __restrict__ oerec, ERec* __restrict__ nerec, uint32_t rs, uint64_t mb,
+                             uint32_t epoch)
 {
     const RunInfo* __restrict__ runs = rx.runs;
     extern __shared__ uint32_t s_tab[];   // LDS: src[k + 1] (sentinel ~0), shift[k + 1]
@@ -893,16 +931,16 @@ __global__ __launch_bounds__(LDS ? 1024 : 256) void k_move_edges(const uint32_t*
             const uint64_t np = insert ? e + shift : e - shift;
             if (np >= cap) continue;
             nadj[np] = x;
-            if (nanc) nanc[np] = anc[e];
-            if (nerec) nerec[np] = patch(oerec[e]);
+            if (nanc) nanc[np * as_out] = anc[e * as_in];
+            if (nerec) nerec[np * rs] = patch(oerec[e * rs]);
             continue;
         }
         // last source run whose row starts at or before e
         const uint64_t lo = run_upper_off(rx, e);
         if (lo == 0) {
             nadj[e] = x;
-            if (nanc) nanc[e] = anc[e];
-            if (nerec) nerec[e] = patch(oerec[e]);
+            if (nanc) nanc[e * as_out] = anc[e * as_in];
+            if (nerec) nerec[e * rs] = patch(oerec[e * rs]);
             continue;
         }
         const RunInfo ri = runs[lo - 1];
@@ -918,31 +956,36 @@ __global__ __launch_bounds__(LDS ? 1024 : 256) void k_move_edges(const uint32_t*
             const uint64_t np = noff[ri.src] + (e - ri.off) + (insert ? before : -(int64_t)before);
             if (np >= cap) continue;   // never taken for a consistent CSR; keeps a bad input in bounds
             nadj[np] = x;
-            if (nanc) nanc[np] = kAnchorNone64;
+            if (nanc) nanc[np * as_out] = kAnchorNone64;
         } else {
             const uint64_t shift = cf[ri.re];
             const uint64_t np = insert ? e + shift : e - shift;
             if (np >= cap) continue;
             nadj[np] = x;
-            if (nanc) nanc[np] = anc[e];
-            if (nerec) nerec[np] = patch(oerec[e]);
+            if (nanc) nanc[np * as_out] = anc[e * as_in];
+            if (nerec) nerec[np * rs] = patch(oerec[e * rs]);
         }
     }
 }
 
-// records of the rebuilt source rows: erec[slot] = vrec[adj[slot]] (block per run)
+// records of the rebuilt source rows: erec[slot] = vrec[adj[slot]] (block per
+// run); their anchor entries are reset (the source's samplers are)
 __global__ void k_erec_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ noff,
-                            const uint32_t* __restrict__ nadj, const ERec* __restrict__ vrec, ERec* __restrict__ erec)
+                            const uint32_t* __restrict__ nadj, const ERec* __restrict__ vrec, ERec* __restrict__ erec,
+                            uint32_t rs)
 {
     const uint32_t s = runs[blockIdx.x].src;
     const uint64_t b = noff[s], e = noff[s + 1];
-    for (uint64_t j = b + threadIdx.x; j < e; j += blockDim.x) erec[j] = vrec[nadj[j]];
+    for (uint64_t j = b + threadIdx.x; j < e; j += blockDim.x) {
+        erec[j * rs] = vrec[nadj[j]];
+        if (rs == 2) reinterpret_cast<uint64_t*>(erec)[j * kAnchorStride + 2] = kAnchorNone64;
+    }
 }
 
 void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* nadj, const ERec* vrec,
-                      ERec* erec, hipStream_t s)
+                      ERec* erec, uint32_t rs, hipStream_t s)
 {
-    if (k) hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, noff, nadj, vrec, erec);
+    if (k) hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, noff, nadj, vrec, erec, rs);
 }
 
 // Place the inserted edges (insert only).
@@ -950,7 +993,7 @@ __global__ void k_place_new(const uint64_t* __restrict__ bkeys, uint64_t mb, con
                             const uint32_t* __restrict__ cf, const uint32_t* __restrict__ run_start, uint64_t k,
                             const RunInfo* __restrict__ runs, const uint32_t* __restrict__ adj,
                             const uint64_t* __restrict__ noff, uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc,
-                            uint64_t cap)
+                            uint32_t as_out, uint64_t cap)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mb; i += (uint64_t)gridDim.x * blockDim.x) {
         if (!chg[i]) continue;
@@ -969,7 +1012,7 @@ __global__ void k_place_new(const uint64_t* __restrict__ bkeys, uint64_t mb, con
         const uint64_t np = noff[ri.src] + (cf[i] - cf[ri.rs]) + (b - ri.off);
         if (np >= cap) continue;
         nadj[np] = d;
-        if (nanc) nanc[np] = kAnchorNone64;
+        if (nanc) nanc[np * as_out] = kAnchorNone64;
     }
 }
 
@@ -1222,10 +1265,10 @@ void launch_run_tables(const RunInfo* runs, uint64_t k, const uint32_t* cf, uint
 void launch_new_offsets(const uint64_t* off, uint64_t n, const RunIndex& x, const uint32_t* cf, uint64_t mb, int insert,
                         uint64_t* noff, hipStream_t s)
 { hipLaunchKernelGGL(k_new_offsets, grid_for(n + 1, 256), 256, 0, s, off, n, x, cf, mb, insert, noff); }
-void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, const RunIndex& x,
+void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint32_t as_in, uint64_t m, const RunIndex& x,
                        const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
-                       uint64_t* nanc, uint64_t cap, const ERec* oerec, ERec* nerec, uint64_t mb, uint32_t epoch,
-                       hipStream_t s)
+                       uint64_t* nanc, uint32_t as_out, uint64_t cap, const ERec* oerec, ERec* nerec, uint32_t rs,
+                       uint64_t mb, uint32_t epoch, hipStream_t s)
 {
     if (!m) return;
     static int max_lds = -1;   // LDS per workgroup (160 KiB on gfx950); two workgroups per CU
@@ -1239,17 +1282,17 @@ void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint64_t m, con
     if ((x.k + 1) * 8 <= (uint64_t)max_lds && !(no_lds && *no_lds == '1')) {
         const size_t lds = (size_t)(x.k + 1) * 8;
         const unsigned grid = (unsigned)std::min<uint64_t>((m + 1023) / 1024, (uint64_t)cu_count() * 2);
-        hipLaunchKernelGGL(k_move_edges<true>, grid, 1024, lds, s, adj, anc, m, x, bkeys, cf, noff, insert, nadj, nanc,
-                           cap, oerec, nerec, mb, epoch);
+        hipLaunchKernelGGL(k_move_edges<true>, grid, 1024, lds, s, adj, anc, as_in, m, x, bkeys, cf, noff, insert, nadj,
+                           nanc, as_out, cap, oerec, nerec, rs, mb, epoch);
     } else {
-        hipLaunchKernelGGL(k_move_edges<false>, grid_for(m, 256), 256, 0, s, adj, anc, m, x, bkeys, cf, noff, insert,
-                           nadj, nanc, cap, oerec, nerec, mb, epoch);
+        hipLaunchKernelGGL(k_move_edges<false>, grid_for(m, 256), 256, 0, s, adj, anc, as_in, m, x, bkeys, cf, noff,
+                           insert, nadj, nanc, as_out, cap, oerec, nerec, rs, mb, epoch);
     }
 }
 void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf, const uint32_t* run_start,
                       uint64_t k, const RunInfo* runs, const uint32_t* adj, const uint64_t* noff, uint32_t* nadj,
-                      uint64_t* nanc, uint64_t cap, hipStream_t s)
-{ hipLaunchKernelGGL(k_place_new, grid_for(mb, 256), 256, 0, s, bkeys, mb, chg, cf, run_start, k, runs, adj, noff, nadj, nanc, cap); }
+                      uint64_t* nanc, uint32_t as_out, uint64_t cap, hipStream_t s)
+{ hipLaunchKernelGGL(k_place_new, grid_for(mb, 256), 256, 0, s, bkeys, mb, chg, cf, run_start, k, runs, adj, noff, nadj, nanc, as_out, cap); }
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s)
 {
     if (!W) return;

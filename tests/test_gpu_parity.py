@@ -261,8 +261,11 @@ def test_rewalk_paths_lockstep_and_deferred(W, monkeypatch, lockstep_min, mode):
     phased sweep (WHARF_LOCKSTEP_MIN=0) and the compacted deferred list (=65:
     every wave defers)."""
     monkeypatch.setenv("WHARF_LOCKSTEP_MIN", lockstep_min)
-    # the CSR move's two record-patch paths (source table in LDS / bucketed L2 table)
+    # the CSR move's two record-patch paths (source table in LDS / bucketed L2
+    # table), and the records rebuilt by a gather (no room for a second record
+    # buffer: node2vec anchors kept aside and merged back)
     monkeypatch.setenv("WHARF_MOVE_NO_LDS", "1" if lockstep_min == "65" else "0")
+    monkeypatch.setenv("WHARF_FORCE_RECORD_REBUILD", "1" if lockstep_min == "65" else "0")
     base = O.generate_batch_of_edges(50000, 1 << 13, 6, False, False)
     off, adj = O.csr_from_edges(1 << 12, base)
     batches = [(True, O.generate_batch_of_edges(800, 1 << 12, 11, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
