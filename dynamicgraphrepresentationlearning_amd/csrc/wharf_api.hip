@@ -86,7 +86,7 @@ struct wharf_handle {
     DevBuf off, adj, vrec, erec, row_epoch, off2, adj2, anchor2, ehash, erec2;
     uint64_t ehash_mask = 0, ehash_used = 0;   // capacity - 1; occupied slots incl. tombstones
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
-    DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, rtabs, count, pairs, sel, defer;
+    DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, rtabs, count, pairs, sel, defer, esave;
     wharf_stats st{};
     std::string err;
 
@@ -304,7 +304,7 @@ void free_handle(wharf_handle* h)
     if (h->s) (void)hipStreamSynchronize(h->s);
     for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
                       &h->aff, &h->rtab, &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags,
-                      &h->chg, &h->cf, &h->runstart, &h->runs, &h->rtabs, &h->count, &h->pairs, &h->sel, &h->defer})
+                      &h->chg, &h->cf, &h->runstart, &h->runs, &h->rtabs, &h->count, &h->pairs, &h->sel, &h->defer, &h->esave})
         b->release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -426,38 +426,59 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->rtabs.ensure(run_tables_words(h->n, h->m) * 4);
         launch_run_tables(h->runs.as<RunInfo>(), k, h->cf.as<uint32_t>(), mb, h->n, h->m, h->rtabs.as<uint32_t>(), &rx, s);
         launch_new_offsets(h->off.as<uint64_t>(), h->n, rx, h->cf.as<uint32_t>(), mb, insert, h->off2.as<uint64_t>(), s);
-        // edge records (node2vec MH: with their anchor entries) move with their
-        // slot and are patched arithmetically when a second record buffer fits;
-        // otherwise they are rebuilt by a gather and the anchors travel through
-        // a separate 8-B-per-slot buffer
+        // Edge records (node2vec MH: with their anchor entries) move with their
+        // slot and are patched arithmetically: into a second record buffer when
+        // it fits, else in place (chunked, k_move_records_inplace) when the
+        // buffer has room for m_new; else they are rebuilt by a gather and the
+        // anchors travel through a separate 8-B-per-slot buffer.
+        // WHARF_FORCE_RECORD_REBUILD (tests): 1 = no second buffer, 2 = gather.
         const uint64_t rs = h->rec_stride();
-        const char* force = getenv("WHARF_FORCE_RECORD_REBUILD");   // tests: the no-room path
-        bool patch = !(force && *force == '1');
-        if (patch) {
+        const uint64_t rec_bytes = std::max<uint64_t>(m_new, 1) * sizeof(ERec) * rs;
+        const char* force = getenv("WHARF_FORCE_RECORD_REBUILD");
+        const int forced = force ? atoi(force) : 0;
+        enum { kPatch, kInPlace, kGather } path = forced ? kInPlace : kPatch;
+        if (path == kPatch) {
             try {
-                h->erec2.ensure(std::max<uint64_t>(m_new, 1) * sizeof(ERec) * rs, true);
+                h->erec2.ensure(rec_bytes, true);
             } catch (const WharfError&) {
                 (void)hipGetLastError();
-                patch = false;
+                path = kInPlace;
             }
         }
-        if (!patch && h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8, true);
+        if (path == kInPlace && (forced == 2 || h->erec.cap < rec_bytes)) path = kGather;
+        if (path == kInPlace) {
+            const uint64_t C = inplace_chunk(total_chg);
+            try {
+                h->esave.ensure(std::max<uint64_t>((h->m + C - 1) / C * total_chg, 1) * sizeof(ERec) * rs);
+            } catch (const WharfError&) {
+                (void)hipGetLastError();
+                path = kGather;
+            }
+        }
+        if (path == kGather && h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8, true);
         uint64_t* anc_in = h->anchors ? h->erec.as<uint64_t>() + 2 : nullptr;
-        uint64_t* anc_out = !h->anchors ? nullptr : patch ? h->erec2.as<uint64_t>() + 2 : h->anchor2.as<uint64_t>();
-        const uint32_t as_out = patch ? (uint32_t)kAnchorStride : 1u;
-        launch_move_edges(h->adj.as<uint32_t>(), anc_in, kAnchorStride, h->m, rx, bkeys, h->cf.as<uint32_t>(),
+        uint64_t* anc_out = !h->anchors || path == kInPlace ? nullptr
+                            : path == kPatch ? h->erec2.as<uint64_t>() + 2 : h->anchor2.as<uint64_t>();
+        const uint32_t as_out = path == kPatch ? (uint32_t)kAnchorStride : 1u;
+        const uint64_t m_old = h->m;
+        launch_move_edges(h->adj.as<uint32_t>(), anc_in, kAnchorStride, m_old, rx, bkeys, h->cf.as<uint32_t>(),
                           h->off2.as<uint64_t>(), insert, h->adj2.as<uint32_t>(), anc_out, as_out, m_new,
-                          patch ? h->erec.as<ERec>() : nullptr, patch ? h->erec2.as<ERec>() : nullptr, (uint32_t)rs, mb,
-                          h->epoch, s);
+                          path == kPatch ? h->erec.as<ERec>() : nullptr, path == kPatch ? h->erec2.as<ERec>() : nullptr,
+                          (uint32_t)rs, mb, h->epoch, s);
         if (insert)   // (the records of source rows, new slots included, are rebuilt below)
             launch_place_new(bkeys, mb, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(), h->runstart.as<uint32_t>(), k,
                              h->runs.as<RunInfo>(), h->adj.as<uint32_t>(), h->off2.as<uint64_t>(),
-                             h->adj2.as<uint32_t>(), patch ? nullptr : anc_out, 1u, m_new, s);
+                             h->adj2.as<uint32_t>(), path == kGather ? anc_out : nullptr, 1u, m_new, s);
         std::swap(h->off, h->off2);
         std::swap(h->adj, h->adj2);
         h->m = m_new;
-        if (patch) {
-            std::swap(h->erec, h->erec2);
+        if (path == kPatch || path == kInPlace) {
+            if (path == kPatch) {
+                std::swap(h->erec, h->erec2);
+            } else {
+                launch_move_records_inplace(h->erec.as<ERec>(), (uint32_t)rs, m_old, total_chg, h->esave.as<ERec>(), rx,
+                                            h->cf.as<uint32_t>(), mb, insert, h->epoch, s);
+            }
             launch_vrec(h->off.as<uint64_t>(), h->n, h->row_epoch.as<uint32_t>(), h->vrec.as<ERec>(), s);
             launch_erec_rows(h->runs.as<RunInfo>(), k, h->off.as<uint64_t>(), h->adj.as<uint32_t>(),
                              h->vrec.as<ERec>(), h->erec.as<ERec>(), (uint32_t)rs, s);
@@ -950,7 +971,7 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     r.edge_hash_bytes = h->ehash.cap;
     r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->anchor2.cap + h->erec2.cap;
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
-                      h->runs.cap + h->rtabs.cap + h->count.cap + h->pairs.cap + h->sel.cap + h->defer.cap + h->rtab.cap +
+                      h->runs.cap + h->rtabs.cap + h->count.cap + h->pairs.cap + h->sel.cap + h->defer.cap + h->esave.cap + h->rtab.cap +
                       h->bitmap.cap + h->counters.cap + h->errflag.cap;
     r.total_bytes = r.csr_bytes + r.records_bytes + r.walks_bytes + r.samplers_bytes + r.edge_hash_bytes +
                     r.update_buffers_bytes + r.scratch_bytes;

@@ -91,6 +91,10 @@ void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint32_t as_in,
                        const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
                        uint64_t* nanc, uint32_t as_out, uint64_t cap, const ERec* oerec, ERec* nerec, uint32_t rs,
                        uint64_t mb, uint32_t epoch, hipStream_t s);
+uint64_t move_lds_limit();
+uint64_t inplace_chunk(uint64_t S);   // slots per chunk of the in-place record move (the save buffer holds S per chunk)
+void launch_move_records_inplace(ERec* rec, uint32_t rs, uint64_t m, uint64_t S, ERec* save, const RunIndex& x,
+                                 const uint32_t* cf, uint64_t mb, int insert, uint32_t epoch, hipStream_t s);
 void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* nadj, const ERec* vrec,
                       ERec* erec, uint32_t rs, hipStream_t s);
 void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf,

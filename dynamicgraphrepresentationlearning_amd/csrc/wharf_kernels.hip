@@ -876,6 +876,40 @@ __device__ __forceinline__ ERec patch_rec(const ERec r, const RunIndex& x, const
     return make_rec(v, deg, off, ep);
 }
 
+// The source ids and their row shifts in LDS (k + 1 entries each, ~0 sentinel).
+__device__ __forceinline__ void run_table_to_lds(const RunIndex& rx, const uint32_t* __restrict__ cf, uint64_t mb,
+                                                 uint32_t* s_tab)
+{
+    const uint32_t k = (uint32_t)rx.k;
+    for (uint32_t j = threadIdx.x; j <= k; j += blockDim.x) {
+        s_tab[j] = j < k ? rx.runs[j].src : ~0u;
+        s_tab[k + 1 + j] = cf[j < k ? rx.runs[j].rs : mb];
+    }
+    __syncthreads();
+}
+
+// patch_rec with the source search in LDS
+__device__ __forceinline__ ERec patch_rec_lds(const ERec r, const RunIndex& rx, const uint32_t* s_tab,
+                                              const uint32_t* __restrict__ cf, int insert, uint32_t epoch)
+{
+    const uint32_t k = (uint32_t)rx.k;
+    uint32_t lo = 0, hi = k;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_tab[mid] < r.v) lo = mid + 1; else hi = mid;
+    }
+    const uint64_t shift = s_tab[k + 1 + lo];
+    uint64_t off = r.oe & kOffMask;
+    uint32_t ep = (uint32_t)(r.oe >> kOffBits), deg = r.deg;
+    off = insert ? off + shift : off - shift;
+    if (s_tab[lo] == r.v) {   // a batch source (rare): degree change, sampler reset
+        const uint32_t d = cf[rx.runs[lo].re] - cf[rx.runs[lo].rs];
+        deg = insert ? deg + d : deg - d;
+        ep = epoch;
+    }
+    return make_rec(r.v, deg, off, ep);
+}
+
 // LDS = true (up to 10 k source runs, 80 KiB): the source ids and their row
 // shifts sit in LDS, so the target-record patch is a binary search in LDS
 // instead of a random L2 lookup per edge (random lookups, even L2 hits, cap
@@ -894,34 +928,10 @@ __global__ __launch_bounds__(LDS ? 1024 : 256) void k_move_edges(const uint32_t*
 {
     const RunInfo* __restrict__ runs = rx.runs;
     extern __shared__ uint32_t s_tab[];   // LDS: src[k + 1] (sentinel ~0), shift[k + 1]
-    const uint32_t k = (uint32_t)rx.k;
-    if constexpr (LDS) {
-        for (uint32_t j = threadIdx.x; j <= k; j += blockDim.x) {
-            s_tab[j] = j < k ? runs[j].src : ~0u;
-            s_tab[k + 1 + j] = cf[j < k ? runs[j].rs : mb];
-        }
-        __syncthreads();
-    }
+    if constexpr (LDS) run_table_to_lds(rx, cf, mb, s_tab);
     auto patch = [&](const ERec r) -> ERec {
-        if constexpr (!LDS) {
-            return patch_rec(r, rx, cf, mb, insert, epoch);
-        } else {
-            uint32_t lo = 0, hi = k;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_tab[mid] < r.v) lo = mid + 1; else hi = mid;
-            }
-            const uint64_t shift = s_tab[k + 1 + lo];
-            uint64_t off = r.oe & kOffMask;
-            uint32_t ep = (uint32_t)(r.oe >> kOffBits), deg = r.deg;
-            off = insert ? off + shift : off - shift;
-            if (s_tab[lo] == r.v) {   // a batch source (rare): degree change, sampler reset
-                const uint32_t d = cf[runs[lo].re] - cf[runs[lo].rs];
-                deg = insert ? deg + d : deg - d;
-                ep = epoch;
-            }
-            return make_rec(r.v, deg, off, ep);
-        }
+        if constexpr (!LDS) return patch_rec(r, rx, cf, mb, insert, epoch);
+        else return patch_rec_lds(r, rx, s_tab, cf, insert, epoch);
     };
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t x = adj[e];
@@ -966,6 +976,163 @@ __global__ __launch_bounds__(LDS ? 1024 : 256) void k_move_edges(const uint32_t*
             if (nerec) nerec[np * rs] = patch(oerec[e * rs]);
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// In-place record move, for graphs whose second record buffer does not fit
+// (configs[4]: 3.6 G slots x 32 B = 115 GB).  Every old slot e outside the
+// batch sources' rows moves to e + sh(e) (insert) or e - sh(e) (delete), sh
+// non-decreasing in e and at most S = the batch's changed edges; the rows of
+// batch sources are rebuilt afterwards (k_erec_rows).  The records are cut in
+// chunks of C >= S slots, one workgroup per chunk:
+//   * insert: a chunk's records land in the chunk itself or in the first S
+//     slots (the head) of the next chunk.  k_save_edges copies every head
+//     aside first; each workgroup then sweeps its chunk from the top down in
+//     tiles (read the tile - its head from the copy - barrier, write), so a
+//     slot is never overwritten before it is read.
+//   * delete: the mirror image (tails saved, tiles bottom up).
+// Destinations are distinct (the move is the CSR's slot permutation), so the
+// only hazard is read-after-overwrite, which the saved heads / tails and the
+// sweep direction exclude.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t moved_slot(const RunIndex& rx, const uint32_t* __restrict__ cf, int insert, uint64_t e)
+{
+    const uint32_t es = rx.eshift[e >> rx.es];
+    if (es >> 31) {
+        const uint64_t sh = es & 0x7FFFFFFFu;
+        return insert ? e + sh : e - sh;
+    }
+    const uint64_t lo = run_upper_off(rx, e);
+    if (lo == 0) return e;
+    const RunInfo ri = rx.runs[lo - 1];
+    if (e < ri.end) return ~0ull;   // in a source row: rebuilt
+    const uint64_t sh = cf[ri.re];
+    return insert ? e + sh : e - sh;
+}
+
+__device__ __forceinline__ void copy_rec(const ERec* __restrict__ src, ERec* __restrict__ dst, uint32_t rs)
+{
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    d4[0] = s4[0];
+    if (rs == 2) d4[1] = s4[1];
+}
+
+// the slots of chunk c that the neighbouring chunk writes into: head [lo, lo + S)
+// for inserts (c > 0), tail [hi - S, hi) for deletes (c < last)
+__device__ __forceinline__ bool saved_region(uint64_t c, uint64_t nchunks, uint64_t C, uint64_t S, uint64_t m,
+                                             int insert, uint64_t& b0)
+{
+    const uint64_t lo = c * C, hi = lo + C < m ? lo + C : m;
+    if (insert) {
+        b0 = lo;
+        return c > 0 && S > 0;
+    }
+    b0 = hi > S ? hi - S : 0;
+    return c + 1 < nchunks && S > 0;
+}
+
+__global__ void k_save_edges(const ERec* __restrict__ rec, uint32_t rs, uint64_t m, uint64_t C, uint64_t S, int insert,
+                             ERec* __restrict__ save)
+{
+    const uint64_t nchunks = (m + C - 1) / C;
+    const uint64_t total = nchunks * S;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = i / S, j = i - c * S;
+        uint64_t b0;
+        if (!saved_region(c, nchunks, C, S, m, insert, b0)) continue;
+        if (b0 + j < m) copy_rec(rec + (b0 + j) * rs, save + i * rs, rs);
+    }
+}
+
+// each thread moves kInplaceR records per tile (independent loads in flight)
+constexpr uint32_t kInplaceR = 4;
+
+template <bool INSERT, bool LDS>
+__global__ __launch_bounds__(1024) void k_move_records_inplace(ERec* __restrict__ rec, uint32_t rs, uint64_t m,
+                                                               uint64_t C, uint64_t S, const ERec* __restrict__ save,
+                                                               RunIndex rx, const uint32_t* __restrict__ cf,
+                                                               uint64_t mb, uint32_t epoch)
+{
+    extern __shared__ uint32_t s_tab[];
+    if constexpr (LDS) run_table_to_lds(rx, cf, mb, s_tab);
+    const uint64_t nchunks = (m + C - 1) / C;
+    const uint64_t c = blockIdx.x;
+    const uint64_t lo = c * C, hi = lo + C < m ? lo + C : m;
+    uint64_t b0;
+    const bool has_saved = saved_region(c, nchunks, C, S, m, INSERT, b0);
+    const uint64_t tsz = (uint64_t)blockDim.x * kInplaceR;
+    const uint64_t ntile = (hi - lo + tsz - 1) / tsz;
+    for (uint64_t t = 0; t < ntile; t++) {
+        const uint64_t tile = INSERT ? ntile - 1 - t : t;
+        uint64_t np[kInplaceR];
+        uint4 q0[kInplaceR], q1[kInplaceR];
+#pragma unroll
+        for (uint32_t k = 0; k < kInplaceR; k++) {
+            const uint64_t e = lo + tile * tsz + k * blockDim.x + threadIdx.x;
+            np[k] = ~0ull;
+            q0[k] = q1[k] = make_uint4(0, 0, 0, 0);
+            if (e < hi) {
+                np[k] = moved_slot(rx, cf, INSERT, e);
+                if (np[k] != ~0ull) {
+                    const bool from_save = has_saved && e >= b0 && e < b0 + S;
+                    const uint4* src =
+                        reinterpret_cast<const uint4*>(from_save ? save + (c * S + (e - b0)) * rs : rec + e * rs);
+                    q0[k] = src[0];
+                    if (rs == 2) q1[k] = src[1];
+                }
+            }
+        }
+        __syncthreads();   // every read of this tile before any write
+#pragma unroll
+        for (uint32_t k = 0; k < kInplaceR; k++) {
+            if (np[k] == ~0ull) continue;
+            ERec r;
+            r.v = q0[k].x;
+            r.deg = q0[k].y;
+            r.oe = ((uint64_t)q0[k].w << 32) | q0[k].z;
+            const ERec pr = LDS ? patch_rec_lds(r, rx, s_tab, cf, INSERT, epoch) : patch_rec(r, rx, cf, mb, INSERT, epoch);
+            uint4* dst = reinterpret_cast<uint4*>(rec + np[k] * rs);
+            dst[0] = make_uint4(pr.v, pr.deg, (uint32_t)pr.oe, (uint32_t)(pr.oe >> 32));
+            if (rs == 2) dst[1] = q1[k];   // the anchor entry travels with its slot
+        }
+    }
+}
+
+uint64_t inplace_chunk(uint64_t S) { return std::max<uint64_t>(1ull << 20, S); }
+
+// bytes of LDS a 1024-thread record-move workgroup may hold its source table in
+// (two workgroups per CU; 0 with WHARF_MOVE_NO_LDS=1, for tests)
+uint64_t move_lds_limit()
+{
+    static int max_lds = -1;
+    if (max_lds < 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) max_lds = 65536;
+        max_lds = std::min(max_lds, 80 * 1024);
+    }
+    const char* no_lds = getenv("WHARF_MOVE_NO_LDS");
+    return (no_lds && *no_lds == '1') ? 0 : (uint64_t)max_lds;
+}
+
+void launch_move_records_inplace(ERec* rec, uint32_t rs, uint64_t m, uint64_t S, ERec* save, const RunIndex& x,
+                                 const uint32_t* cf, uint64_t mb, int insert, uint32_t epoch, hipStream_t s)
+{
+    if (!m) return;
+    const uint64_t C = inplace_chunk(S);
+    const uint64_t nchunks = (m + C - 1) / C;
+    if (S) hipLaunchKernelGGL(k_save_edges, grid_for(nchunks * S, 256), 256, 0, s, rec, rs, m, C, S, insert, save);
+    const size_t lds = (size_t)(x.k + 1) * 8;
+    const bool in_lds = lds <= move_lds_limit();
+#define WHARF_INPLACE(I, D) \
+    hipLaunchKernelGGL((k_move_records_inplace<I, D>), (unsigned)nchunks, 1024, D ? lds : 0, s, rec, rs, m, C, S, save, x, cf, mb, epoch)
+    if (insert) {
+        if (in_lds) WHARF_INPLACE(true, true); else WHARF_INPLACE(true, false);
+    } else {
+        if (in_lds) WHARF_INPLACE(false, true); else WHARF_INPLACE(false, false);
+    }
+#undef WHARF_INPLACE
 }
 
 // records of the rebuilt source rows: erec[slot] = vrec[adj[slot]] (block per
@@ -1271,15 +1438,7 @@ void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint32_t as_in,
                        uint64_t mb, uint32_t epoch, hipStream_t s)
 {
     if (!m) return;
-    static int max_lds = -1;   // LDS per workgroup (160 KiB on gfx950); two workgroups per CU
-    if (max_lds < 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) max_lds = 65536;
-        max_lds = std::min(max_lds, 80 * 1024);
-    }
-    const char* no_lds = getenv("WHARF_MOVE_NO_LDS");   // tests: force the L2-table path
-    if ((x.k + 1) * 8 <= (uint64_t)max_lds && !(no_lds && *no_lds == '1')) {
+    if ((x.k + 1) * 8 <= move_lds_limit()) {
         const size_t lds = (size_t)(x.k + 1) * 8;
         const unsigned grid = (unsigned)std::min<uint64_t>((m + 1023) / 1024, (uint64_t)cu_count() * 2);
         hipLaunchKernelGGL(k_move_edges<true>, grid, 1024, lds, s, adj, anc, as_in, m, x, bkeys, cf, noff, insert, nadj,

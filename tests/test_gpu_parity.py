@@ -253,19 +253,26 @@ def test_affected_ids_on_device_match_host_list(W):
     gd.destroy()
 
 
-@pytest.mark.parametrize("lockstep_min", ["0", "65"])
+# (WHARF_LOCKSTEP_MIN, WHARF_MOVE_NO_LDS, WHARF_FORCE_RECORD_REBUILD)
+PATHS = {"sweep/patch-lds": ("0", "0", "0"), "deferred/inplace-l2": ("65", "1", "1"),
+         "mixed/inplace-lds": ("40", "0", "1"), "mixed/gather": ("16", "1", "2")}
+
+
+@pytest.mark.parametrize("path", list(PATHS))
 @pytest.mark.parametrize("mode", ["det", "deepwalk", "node2vec"])
-def test_rewalk_paths_lockstep_and_deferred(W, monkeypatch, lockstep_min, mode):
-    """Every re-walk kernel reproduces the oracle's corpus, counters and affected
-    ids: the interleaved sweep (DeepWalk, deterministic), and for node2vec the
-    phased sweep (WHARF_LOCKSTEP_MIN=0) and the compacted deferred list (=65:
-    every wave defers)."""
+def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
+    """Every re-walk kernel and every CSR-update path reproduces the oracle's
+    corpus, counters, affected ids and CSR.  Re-walk: the interleaved sweep
+    (DeepWalk, deterministic); for node2vec the phased sweep
+    (WHARF_LOCKSTEP_MIN=0), the compacted deferred list (=65: every wave
+    defers) and a mix.  CSR update: the record patch with the source table in
+    LDS or the bucketed L2 table (WHARF_MOVE_NO_LDS), into a second record
+    buffer, in place (chunked), or records rebuilt by a gather with node2vec
+    anchors kept aside (WHARF_FORCE_RECORD_REBUILD=1 / 2)."""
+    lockstep_min, no_lds, force = PATHS[path]
     monkeypatch.setenv("WHARF_LOCKSTEP_MIN", lockstep_min)
-    # the CSR move's two record-patch paths (source table in LDS / bucketed L2
-    # table), and the records rebuilt by a gather (no room for a second record
-    # buffer: node2vec anchors kept aside and merged back)
-    monkeypatch.setenv("WHARF_MOVE_NO_LDS", "1" if lockstep_min == "65" else "0")
-    monkeypatch.setenv("WHARF_FORCE_RECORD_REBUILD", "1" if lockstep_min == "65" else "0")
+    monkeypatch.setenv("WHARF_MOVE_NO_LDS", no_lds)
+    monkeypatch.setenv("WHARF_FORCE_RECORD_REBUILD", force)
     base = O.generate_batch_of_edges(50000, 1 << 13, 6, False, False)
     off, adj = O.csr_from_edges(1 << 12, base)
     batches = [(True, O.generate_batch_of_edges(800, 1 << 12, 11, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
