@@ -85,21 +85,54 @@ __device__ __forceinline__ float weight(const WalkArgs& a, const Row& rprev, uin
 
 // MetropolisHastingsSampler::init (metropolis_hastings_sampler.h:69-108) with
 // proposals from the (cur, prev, epoch of cur's row) Philox stream.  Returns
-// the anchor as a slot of cur's row.
-__device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp)
+// the anchor as a slot of cur's row, and its weight class.
+//
+// WEIGHT (best of 1 + 20 proposals, strict '>', so the first maximum wins):
+// the proposals' targets are loaded in groups of 8 independent reads, and
+// has_edge is asked only while it can still matter — once the best weight
+// reaches max(1, 1/q) only a return proposal (c == prev, no lookup) can beat
+// it.  Same result as the sequential loop, a fraction of its dependent reads
+// (configs[4] node2vec re-walks init an anchor every 4th step).
+constexpr uint32_t kWeightProposals = 21, kProposalGroup = 4;
+
+__device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp, uint32_t& cls)
 {
     const uint32_t ep = rc.epoch << 4;
+    if (a.init == kInitWeight) {
+        const float wtop = fmaxf(1.0f, a.inv_q);   // best weight a non-return proposal can have
+        float best = 0.0f;
+        uint32_t last = 0, lcls = 2;
+        for (uint32_t g = 0; g < kWeightProposals; g += kProposalGroup) {
+            uint32_t slot[kProposalGroup], cv[kProposalGroup];
+#pragma unroll
+            for (uint32_t k = 0; k < kProposalGroup; k++) {
+                const uint32_t j = g + k < kWeightProposals ? g + k : kWeightProposals - 1;
+                const P4 r = philox4x32_10(rc.v, rp.v, j, ep | kStreamAnchor, a.key0, a.key1);
+                slot[k] = (uint32_t)pick32(r.x0, rc.deg);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kProposalGroup; k++) cv[k] = a.adj[rc.off + slot[k]];
+#pragma unroll
+            for (uint32_t k = 0; k < kProposalGroup; k++) {
+                const uint32_t j = g + k;
+                if (j >= kWeightProposals) break;
+                uint32_t c;
+                if (cv[k] == rp.v) {
+                    c = 0;
+                } else {
+                    if (j > 0 && best >= wtop) continue;   // cannot be strictly greater
+                    c = has_edge(a, rp, cv[k]) ? 1 : 2;
+                }
+                const float w = class_weight(a, c);
+                if (j == 0 || w > best) { best = w; last = slot[k]; lcls = c; }
+            }
+        }
+        cls = lcls;
+        return last;
+    }
     P4 r = philox4x32_10(rc.v, rp.v, 0, ep | kStreamAnchor, a.key0, a.key1);
     uint32_t last = (uint32_t)pick32(r.x0, rc.deg);
-    if (a.init == kInitWeight) {
-        float best = weight<kNode2Vec>(a, rp, a.adj[rc.off + last]);
-        for (uint32_t j = 1; j <= 20; j++) {
-            r = philox4x32_10(rc.v, rp.v, j, ep | kStreamAnchor, a.key0, a.key1);
-            const uint32_t cand = (uint32_t)pick32(r.x0, rc.deg);
-            const float w = weight<kNode2Vec>(a, rp, a.adj[rc.off + cand]);
-            if (w > best) { best = w; last = cand; }
-        }
-    } else if (a.init == kInitBurnin) {
+    if (a.init == kInitBurnin) {
         for (uint32_t i = 0; i < 100; i++) {
             r = philox4x32_10(rc.v, rp.v, i, ep | kStreamBurnin, a.key0, a.key1);
             const uint32_t cand = (uint32_t)pick32(r.x0, rc.deg);
@@ -108,6 +141,7 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp)
             if (wl < wn || u01(r.x1, r.x2) <= (double)wn / (double)wl) last = cand;
         }
     }
+    cls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + last]);
     return last;
 }
 
@@ -136,8 +170,7 @@ __device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc,
             return (uint32_t)anc;
         }
     }
-    const uint32_t an = anchor_init(a, rc, rp);
-    cls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + an]);
+    const uint32_t an = anchor_init(a, rc, rp, cls);
     if (ein >= 0) a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     return an;
 }
