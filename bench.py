@@ -63,6 +63,17 @@ def balanced_shards(deg: np.ndarray, parts: int):
     return bs(deg, parts)
 
 
+def gather_ceiling(steps_per_s: float):
+    """The kernel's binding ceiling: one dependent random 16-B gather per step,
+    at the chip's measured random-gather rate (profiles/gather_ceiling.json)."""
+    path = os.path.join(REPO, "profiles", "gather_ceiling.json")
+    if not os.path.exists(path):
+        return None
+    g = json.load(open(path))
+    return {"Ggathers_per_s": g["Ggathers_per_s"], "frac": round(steps_per_s / (g["Ggathers_per_s"] * 1e9), 4),
+            "source": "profiles/gather_ceiling.json"}
+
+
 def load_traffic(tag: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
     path = os.path.join(REPO, "profiles", f"pmc_{tag}.json")
@@ -292,7 +303,8 @@ def main():
                          "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
                          "traffic": traffic, "bytes_per_step": bytes_per_step,
-                         "avg_kernel_ms": round(avg_kernel_ms, 3)},
+                         "avg_kernel_ms": round(avg_kernel_ms, 3),
+                         "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3))},
             "rewalk_latency_10k_batch": rewalk,
             "corpus_allgatherv": corpus,
             "cpu_baseline": None,
