@@ -113,8 +113,6 @@ unsigned aff_blocks(uint64_t W);
 void launch_aff_count(const uint8_t* aff, uint64_t W, uint32_t* counts, hipStream_t s);
 void launch_aff_write(const uint8_t* aff, uint64_t W, const uint32_t* offs, uint64_t n, uint64_t n_loc, uint64_t lo,
                       uint32_t* out, hipStream_t s);
-void launch_li_to_wid(const uint64_t* li, uint64_t cnt, uint64_t n, uint64_t n_loc, uint64_t lo, uint32_t* out,
-                      hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s);
 void launch_fill_u64(uint64_t* p, uint64_t cnt, uint64_t v, hipStream_t s);
 void launch_edge_hash_update(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, int insert, uint64_t* table,

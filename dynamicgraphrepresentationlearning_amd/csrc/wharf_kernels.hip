@@ -1,12 +1,15 @@
 // HIP kernels of the WharfMH walk engine, written for gfx950 (CDNA4).
 //
-// Layout in HBM (see DESIGN.md):
-//   vrec[n]        {row offset, degree}: one aligned 8-B (16-B when m >= 2^32) load per step
+// Layout in HBM (see DESIGN.md §3):
+//   vrec[n]        16-B row record {v, deg, row offset:40 | row epoch:24}
+//   erec[m]        per CSR slot, its target's row record (one 16-B gather per
+//                  walk step); node2vec MH: 32-B records, bytes 16-23 = the
+//                  slot's frozen-anchor cache entry
 //   adj[m]         u32 targets, rows ascending (the order CompressedEdges::get_edges yields)
 //   walks[L][W]    position-major walk matrix: lane i of a wave owns walk i, so every
 //                  store/load of one position by a wave is one contiguous 256-B segment
-//   anchor[m]      frozen MH anchor per (cur, slot of prev in adj(cur)) (node2vec MH)
-//   bitmap[n/32]   batch-source set for the rewalk-point scan
+//   ehash          node2vec: edge set for has_edge (32-B buckets)
+//   bitmap[n/32]   batch-source set for the rewalk-point scan, + its Bloom filter
 #include <cstdlib>
 
 #include "wharf_kernels.h"
@@ -1375,16 +1378,6 @@ void launch_aff_write(const uint8_t* aff, uint64_t W, const uint32_t* offs, uint
                       uint32_t* out, hipStream_t s)
 { if (W) hipLaunchKernelGGL(k_aff_write, aff_blocks(W), 256, 0, s, aff, W, offs, n, n_loc, lo, out); }
 
-__global__ void k_li_to_wid(const uint64_t* __restrict__ li, uint64_t cnt, uint64_t n, uint64_t n_loc, uint64_t lo,
-                            uint32_t* __restrict__ out)
-{
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t l = li[i];
-        const uint64_t r = l / n_loc;
-        out[i] = (uint32_t)(r * n + lo + (l - r * n_loc));
-    }
-}
-
 __global__ void k_fill_u64(uint64_t* __restrict__ p, uint64_t cnt, uint64_t v)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x)
@@ -1500,8 +1493,6 @@ void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, uint64_
 { hipLaunchKernelGGL(k_index_entries, grid_for(W, 256), 256, 0, s, walks, W, L, n, n_loc, lo, kb, col_base, skeys, vals); }
 void launch_index_split(const uint64_t* skeys, uint64_t E, int kb, unsigned long long* counts, uint64_t* keys, hipStream_t s)
 { hipLaunchKernelGGL(k_index_split, grid_for(E, 256), 256, 0, s, skeys, E, kb, counts, keys); }
-void launch_li_to_wid(const uint64_t* li, uint64_t cnt, uint64_t n, uint64_t n_loc, uint64_t lo, uint32_t* out, hipStream_t s)
-{ if (cnt) hipLaunchKernelGGL(k_li_to_wid, grid_for(cnt, 256), 256, 0, s, li, cnt, n, n_loc, lo, out); }
 void launch_fill_u64(uint64_t* p, uint64_t cnt, uint64_t v, hipStream_t s)
 { if (cnt) hipLaunchKernelGGL(k_fill_u64, grid_for(cnt, 256), 256, 0, s, p, cnt, v); }
 void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s)
