@@ -19,7 +19,9 @@ constexpr uint32_t kAnchorNone = 0xFFFFFFFFu;  // MH anchor slot not initialised
 constexpr uint32_t kNoRewalk = 0xFFu;          // rewalk position "none"
 constexpr uint32_t kBloomWords = 4096;         // batch-source Bloom filter: 2^17 bits (16 KiB, LDS)
 
+// two 17-bit hashes (k = 2: ~2 % false positives at 10 k sources in 2^17 bits)
 __host__ __device__ __forceinline__ uint32_t bloom_hash(uint32_t x) { return (x * 2654435761u) >> 15; }
+__host__ __device__ __forceinline__ uint32_t bloom_hash2(uint32_t x) { return ((x ^ 0x5bd1e995u) * 0x9E3779B1u + 0x7f4a7c15u) >> 15; }
 
 // Philox counter word 3 = (epoch << 4) | stream
 enum : uint32_t { kStreamStep = 0, kStreamAnchor = 1, kStreamBurnin = 2, kStreamPrev = 3 };

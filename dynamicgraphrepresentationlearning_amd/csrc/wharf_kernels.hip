@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
 enum : uint32_t { kLaneScan = 0, kLaneWalk = 1, kLaneDone = 2 };
 
 // Batch-source test of the rewalk-point scan: a 16-KiB Bloom filter of the
-// batch sources (one hash, 2^17 bits: <= 8 % false positives at 10 k sources)
+// batch sources (two hashes, 2^17 bits: ~2 % false positives at 10 k sources)
 // in LDS answers most positions; only its positives read the exact bitmap.
 // Without it every scanned position is a random L2 read of the n-bit bitmap
 // (1.6 G per configs[2] batch, the re-walk kernel's only extra cost over
@@ -331,8 +331,8 @@ __device__ __forceinline__ void bloom_to_lds(const WalkArgs& a, uint32_t* s_bloo
 
 __device__ __forceinline__ bool is_source(const WalkArgs& a, const uint32_t* s_bloom, uint32_t x)
 {
-    const uint32_t h = bloom_hash(x);
-    if (!((s_bloom[h >> 5] >> (h & 31)) & 1u)) return false;
+    const uint32_t h = bloom_hash(x), h2 = bloom_hash2(x);
+    if (!((s_bloom[h >> 5] >> (h & 31)) & (s_bloom[h2 >> 5] >> (h2 & 31)) & 1u)) return false;
     return (a.bitmap[x >> 5] >> (x & 31)) & 1u;
 }
 
@@ -794,8 +794,9 @@ __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* _
         ri.src = s; ri.rs = rs; ri.re = re; ri.off = off[s]; ri.end = off[s + 1];
         runs[j] = ri;
         atomicOr(bitmap + (s >> 5), 1u << (s & 31));
-        const uint32_t h = bloom_hash(s);
+        const uint32_t h = bloom_hash(s), h2 = bloom_hash2(s);
         atomicOr(bloom + (h >> 5), 1u << (h & 31));
+        atomicOr(bloom + (h2 >> 5), 1u << (h2 & 31));
         if (row_epoch) row_epoch[s] = epoch;   // the source's samplers are reset (wharfmh.h:504,539)
     }
 }
