@@ -63,6 +63,7 @@ def lib():
             getattr(L, f).restype = u64
         L.wo_get_csr.argtypes = [p, p, p]
         L.wo_get_walks.argtypes = [p, p]
+        L.wo_get_walks_range.argtypes = [p, u64, u64, p]
         L.wo_export_index.argtypes = [p, p, p, p]
         L.wo_time_generate_range.argtypes = [p, u64, u64, C.c_int]
         L.wo_time_generate_range.restype = C.c_double
@@ -206,6 +207,12 @@ class Engine:
         """[W][L] walk-major, SENT-padded."""
         out = np.zeros((self.num_walks, self.L), dtype=np.uint32)
         lib().wo_get_walks(self._h, _ptr(out))
+        return out
+
+    def walks_range(self, w0: int, w1: int) -> np.ndarray:
+        """walks [w0, w1) of the [W][L] corpus (no copy of the rest)."""
+        out = np.zeros((w1 - w0, self.L), dtype=np.uint32)
+        lib().wo_get_walks_range(self._h, w0, w1, _ptr(out))
         return out
 
     def index(self):

@@ -533,6 +533,11 @@ void wo_get_walks(const wo_engine* e, uint32_t* out)
     memcpy(out, e->walks, e->n * e->wpv * e->L * 4);
 }
 
+void wo_get_walks_range(const wo_engine* e, uint64_t w0, uint64_t w1, uint32_t* out)
+{
+    memcpy(out, e->walks + w0 * e->L, (w1 - w0) * e->L * 4);
+}
+
 /* walks/inverted_index.h:12-37: vertex walk[pos] holds key wid*L+pos -> next
  * (SENT at the last position), per vertex ascending by key. */
 uint64_t wo_index_size(const wo_engine* e)

@@ -73,6 +73,7 @@ uint64_t wo_num_edges(const wo_engine* e);
 uint64_t wo_num_walks(const wo_engine* e);
 void     wo_get_csr(const wo_engine* e, uint64_t* off_out, uint32_t* adj_out);
 void     wo_get_walks(const wo_engine* e, uint32_t* out);   /* [W][L] walk-major */
+void     wo_get_walks_range(const wo_engine* e, uint64_t w0, uint64_t w1, uint32_t* out);   /* walks [w0, w1) */
 uint64_t wo_get_accepts(const wo_engine* e);               /* MH acceptances since last reset */
 uint64_t wo_get_steps(const wo_engine* e);
 /* Inverted index (walks/inverted_index.h:12-93): counts[n], then per vertex
