@@ -47,6 +47,7 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ t, uin
     const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (li >= W) return;
     uint32_t x = mix((uint32_t)li);
+    uint32_t b0 = 0, b1 = 0, b2 = 0;   // mode 8: 4-step store buffer
     for (int p = 0; p < L; p++) {
         uint64_t slot;
         if (MODE == 4) {                                                          // dep + Philox4x32-10 per step
@@ -61,20 +62,39 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ t, uin
             }
             x = c0;
         }
-        if (MODE == 0 || MODE == 4) slot = __umulhi(x, (uint32_t)n);             // dep
+        if (MODE == 0 || MODE >= 4) slot = __umulhi(x, (uint32_t)n);             // dep
         else if (MODE == 1) slot = __umulhi(mix((uint32_t)(li * 131 + p)), (uint32_t)n);   // indep
         else if (MODE == 2) slot = (li + (uint64_t)p * W) % n;                    // stream
         else slot = __umulhi(x, (uint32_t)n);                                     // dep, nt load
         uint4 r;
-        if (MODE == 3) {
+        if (MODE == 5) {          // dep, 4-B loads anywhere in the table
+            const uint32_t* t4 = reinterpret_cast<const uint32_t*>(t);
+            const uint32_t q = t4[__umulhi(x, (uint32_t)n) * 4 + (x & 3)];
+            r = make_uint4(q, q ^ 0x9e3779b9u, 0, 0);
+        } else if (MODE == 6) {   // dep, 8-B loads
+            const uint2* t2 = reinterpret_cast<const uint2*>(t);
+            const uint2 q = t2[__umulhi(x, (uint32_t)n) * 2 + (x & 1)];
+            r = make_uint4(q.x, q.y, 0, 0);
+        } else if (MODE == 3) {
             typedef unsigned int v4u __attribute__((ext_vector_type(4)));
             const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(t + slot));
             r = make_uint4(q.x, q.y, q.z, q.w);
         } else {
             r = t[slot];
         }
-        out[(uint64_t)p * W + li] = r.x;
-        x = (MODE == 0 || MODE == 3 || MODE == 4) ? mix(r.y ^ x) : x + r.y;
+        if (MODE == 8) {          // dep, one 16-B store per 4 steps ([p/4][W] x uint4 layout)
+            if ((p & 3) == 0) b0 = r.x;
+            else if ((p & 3) == 1) b1 = r.x;
+            else if ((p & 3) == 2) b2 = r.x;
+            else reinterpret_cast<uint4*>(out)[(uint64_t)(p >> 2) * W + li] = make_uint4(b0, b1, b2, r.x);
+        } else if (MODE == 9) {   // dep, a store per step into one L2-resident row
+            out[li] = r.x;
+        } else if (MODE == 10) {  // dep, non-temporal store
+            __builtin_nontemporal_store(r.x, out + (uint64_t)p * W + li);
+        } else if (MODE != 7 || r.x == 0xFFFFFFFFu) {
+            out[(uint64_t)p * W + li] = r.x;   // 7: dep without the store
+        }
+        x = (MODE == 0 || MODE >= 3) ? mix(r.y ^ x) : x + r.y;
     }
 }
 
@@ -96,15 +116,23 @@ int main(int argc, char** argv)
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
-    const char* names[5] = {"dep", "indep", "stream", "dep_nt", "dep_philox"};
+    const char* names[11] = {"dep", "indep", "stream", "dep_nt", "dep_philox", "dep_4B", "dep_8B", "dep_nostore",
+                             "dep_store16B_per_4", "dep_store_same_row", "dep_store_nt"};
     for (int rep = 0; rep < 2; rep++)
-        for (int mode = 0; mode < 5; mode++) {
+        for (int mode = 0; mode < 11; mode++) {
+            if (mode >= 1 && mode <= 6) continue;
             CHK(hipEventRecord(a));
             if (mode == 0) hipLaunchKernelGGL(k_gather<0>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 1) hipLaunchKernelGGL(k_gather<1>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 2) hipLaunchKernelGGL(k_gather<2>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 4) hipLaunchKernelGGL(k_gather<4>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 3) hipLaunchKernelGGL(k_gather<3>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 5) hipLaunchKernelGGL(k_gather<5>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 6) hipLaunchKernelGGL(k_gather<6>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 7) hipLaunchKernelGGL(k_gather<7>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 8) hipLaunchKernelGGL(k_gather<8>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 9) hipLaunchKernelGGL(k_gather<9>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 10) hipLaunchKernelGGL(k_gather<10>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             CHK(hipEventRecord(b));
             CHK(hipEventSynchronize(b));
             float ms;
