@@ -29,6 +29,9 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 BYTES_PER_STEP_DEEPWALK = 24     # offsets/deg record 16 B + 1 target 4 B + 1 output 4 B
+# node2vec MH as built: 32-B edge record with the anchor entry + one 32-B has_edge bucket
+# + 4-B output (SURVEY 8(d)'s 44 + 4*ceil(log2 deg) prices the reference's binary search instead)
+BYTES_PER_STEP_NODE2VEC = 68
 ORKUT_EDGES = 117_185_083        # com-orkut undirected edge count (configs[1])
 
 
@@ -196,7 +199,7 @@ def main():
         steps_total, t_max = int(s[0].item()), mx[1].item()
     value = steps_total * args.steps / t_max
     avg_kernel_ms = float(np.mean(kern_ms))
-    bytes_per_step = BYTES_PER_STEP_DEEPWALK if args.model == "deepwalk" else None
+    bytes_per_step = BYTES_PER_STEP_DEEPWALK if args.model == "deepwalk" or args.det else BYTES_PER_STEP_NODE2VEC
     tag = f"gen_{args.model}_{'det' if args.det else 'mh'}_s{args.scale}"
 
     # corpus reassembly for the downstream consumer: full-mesh all-gatherv over RCCL (not timed in `value`)
