@@ -307,7 +307,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
                          "traffic": traffic, "bytes_per_step": bytes_per_step,
                          "avg_kernel_ms": round(avg_kernel_ms, 3),
-                         "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3))},
+                         "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3))
+                         if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None},
             "rewalk_latency_10k_batch": rewalk,
             "corpus_allgatherv": corpus,
             "cpu_baseline": None,
