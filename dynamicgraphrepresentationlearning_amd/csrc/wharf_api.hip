@@ -498,6 +498,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
                 if (insert) h->ehash_used += total_chg;
             }
         }
+        HIPCHK(hipGetLastError());   // a failed launch of the CSR pipeline surfaces here
         HIPCHK(hipEventRecord(h->ev[1], s));
 
         // 5. rewalk points + suffix re-walk in one pass over the walk matrix
@@ -513,6 +514,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             }
             HIPCHK(hipEventRecord(h->ev[2], s));
             launch_walk(a, true, s);
+            HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(h->ev[3], s));
             // ascending affected walk ids: count per block, scan, write
             const unsigned nb = aff_blocks(h->W);
