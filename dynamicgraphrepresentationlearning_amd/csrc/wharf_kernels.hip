@@ -91,11 +91,14 @@ __device__ __forceinline__ float weight(const WalkArgs& a, const Row& rprev, uin
 // the anchor as a slot of cur's row, and its weight class.
 //
 // WEIGHT (best of 1 + 20 proposals, strict '>', so the first maximum wins):
-// the proposals' targets are loaded in groups of 8 independent reads, and
-// has_edge is asked only while it can still matter — once the best weight
-// reaches max(1, 1/q) only a return proposal (c == prev, no lookup) can beat
-// it.  Same result as the sequential loop, a fraction of its dependent reads
-// (configs[4] node2vec re-walks init an anchor every 4th step).
+// the proposals' targets are loaded in groups of independent reads, and
+// has_edge is asked only while it can matter: once the best weight reaches
+// max(1, 1/q) only a return proposal (c == prev, no lookup) can beat it, and
+// with q == 1 triangle and outward weigh the same.  Same result as the
+// sequential loop.  (configs[4] node2vec re-walks init an anchor every 4th
+// step, with ~18 has_edge calls each: triangle and return proposals are rare
+// on RMAT graphs.  Scanning all proposals for a return first, which needs no
+// lookup, cost more than it saved: 151 -> 185 ms.)
 constexpr uint32_t kWeightProposals = 21, kProposalGroup = 4;
 
 __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp, uint32_t& cls)
@@ -124,7 +127,8 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
                     c = 0;
                 } else {
                     if (j > 0 && best >= wtop) continue;   // cannot be strictly greater
-                    c = has_edge(a, rp, cv[k]) ? 1 : 2;
+                    // q == 1: triangle and outward weigh the same, the class cannot matter
+                    c = a.inv_q == 1.0f ? 1u : (has_edge(a, rp, cv[k]) ? 1u : 2u);
                 }
                 const float w = class_weight(a, c);
                 if (j == 0 || w > best) { best = w; last = slot[k]; lcls = c; }

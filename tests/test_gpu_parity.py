@@ -286,14 +286,15 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
 # ---------------------------------------------------------------------------
 # MH mode
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("pq", [(0.5, 2.0), (4.0, 1.0), (2.0, 0.5)])   # BASELINE, reference default, q < 1
 @pytest.mark.parametrize("init", [0, 1, 2])
-def test_mh_node2vec_bit_exact_vs_oracle(W, init):
+def test_mh_node2vec_bit_exact_vs_oracle(W, init, pq):
     base = O.generate_batch_of_edges(40000, 1 << 12, 5, False, False)
     off, adj = O.csr_from_edges(1 << 11, base)
     batches = [(True, O.generate_batch_of_edges(2000, 1 << 11, 1, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
                (False, O.generate_batch_of_edges(1500, 1 << 11, 2, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
                (True, O.generate_batch_of_edges(300, 1 << 11, 3, False, True), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES)]
-    _compare_stream(W, off, adj, batches, wpv=4, L=40, model=1, paramP=0.5, paramQ=2.0, sampler_init=init,
+    _compare_stream(W, off, adj, batches, wpv=4, L=40, model=1, paramP=pq[0], paramQ=pq[1], sampler_init=init,
                     deterministic=False, seed=1234 + init)
 
 
