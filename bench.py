@@ -66,15 +66,36 @@ def balanced_shards(deg: np.ndarray, parts: int):
     return bs(deg, parts)
 
 
-def gather_ceiling(steps_per_s: float):
+def measure_gather_ceiling():
+    """The chip's dependent random 16-B gather rate with the walk kernel's shape,
+    measured on this box by tools/gather_roof (boxes differ by up to ~10 %);
+    None when the probe is not built."""
+    exe = os.path.join(REPO, "tools", "gather_roof")
+    if not os.access(exe, os.X_OK):
+        return None
+    try:
+        r = subprocess.run([exe, "3.48", "coarse", "dep"], capture_output=True, text=True, timeout=180)
+        for line in r.stdout.splitlines():
+            if line.startswith("{"):
+                return float(json.loads(line)["Ggathers_per_s"])
+    except (subprocess.SubprocessError, ValueError, KeyError, OSError):
+        pass
+    return None
+
+
+def gather_ceiling(steps_per_s: float, live: float | None):
     """The kernel's binding ceiling: one dependent random 16-B gather per step,
-    at the chip's measured random-gather rate (profiles/gather_ceiling.json)."""
+    at the random-gather rate measured live on this box (else the committed
+    measurement of another box, profiles/gather_ceiling.json)."""
+    if live:
+        return {"Ggathers_per_s": round(live, 2), "frac": round(steps_per_s / (live * 1e9), 4),
+                "source": "tools/gather_roof dep, this box"}
     path = os.path.join(REPO, "profiles", "gather_ceiling.json")
     if not os.path.exists(path):
         return None
     g = json.load(open(path))
     return {"Ggathers_per_s": g["Ggathers_per_s"], "frac": round(steps_per_s / (g["Ggathers_per_s"] * 1e9), 4),
-            "source": "profiles/gather_ceiling.json"}
+            "source": "profiles/gather_ceiling.json (another box)"}
 
 
 def load_traffic(tag: str):
@@ -281,6 +302,7 @@ def main():
         gs.destroy()
 
     if rank == 0:
+        live_ceiling = measure_gather_ceiling() if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None
         achieved = (steps_local * bytes_per_step / (avg_kernel_ms * 1e-3) / 1e9) if bytes_per_step else None
         traffic = load_traffic(tag)
         line = {
@@ -307,7 +329,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
                          "traffic": traffic, "bytes_per_step": bytes_per_step,
                          "avg_kernel_ms": round(avg_kernel_ms, 3),
-                         "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3))
+                         "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3), live_ceiling)
                          if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None},
             "rewalk_latency_10k_batch": rewalk,
             "corpus_allgatherv": corpus,

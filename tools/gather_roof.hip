@@ -1,6 +1,6 @@
 // Random-gather roof on MI355X: the ceiling the walk kernel is judged against.
 //
-//   hipcc --offload-arch=gfx950 -O3 tools/gather_roof.hip -o tools/gather_roof && tools/gather_roof [GiB]
+//   hipcc --offload-arch=gfx950 -O3 tools/gather_roof.hip -o tools/gather_roof && tools/gather_roof [GiB [kind [mode]]]
 //
 // A table of 16-B records (size like the edge-record array of the com-orkut-sized
 // graph, 3.7 GB) is gathered at uniformly random slots, one lane per "walk",
@@ -107,6 +107,7 @@ int main(int argc, char** argv)
     uint4* t;
     uint32_t* out;
     const char* kind = argc > 2 ? argv[2] : "coarse";
+    const char* only = argc > 3 ? argv[3] : nullptr;   // one mode by name (bench.py: "dep")
     if (!std::strcmp(kind, "uncached")) CHK(hipExtMallocWithFlags((void**)&t, n * 16, hipDeviceMallocUncached));
     else if (!std::strcmp(kind, "fine")) CHK(hipExtMallocWithFlags((void**)&t, n * 16, hipDeviceMallocFinegrained));
     else CHK(hipMalloc(&t, n * 16));
@@ -120,7 +121,7 @@ int main(int argc, char** argv)
                              "dep_store16B_per_4", "dep_store_same_row", "dep_store_nt"};
     for (int rep = 0; rep < 2; rep++)
         for (int mode = 0; mode < 11; mode++) {
-            if (mode >= 1 && mode <= 6) continue;
+            if (only && std::strcmp(only, names[mode]) != 0) continue;
             CHK(hipEventRecord(a));
             if (mode == 0) hipLaunchKernelGGL(k_gather<0>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 1) hipLaunchKernelGGL(k_gather<1>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
