@@ -35,6 +35,7 @@ for s in "$@"; do
              done ;;
     roof)   step gather_roof 300 tools/gather_roof 3.48 ;;
     big)    step bigscale 900 python tools/bigscale.py ;;
+    index)  step index_probe 800 python tools/index_probe.py ;;
     c4)     step c4_stream 1100 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 50 ;;
     c5n2v)  step c5_node2vec 1100 python tools/bigscale.py --model node2vec --wpv 1 --batches 10 --mixed ;;
     det)    step bench_det 900 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
