@@ -85,6 +85,7 @@ SIGNATURES = {
     "wharf_index_size": (_I, [_P, _P]),
     "wharf_export_index": (_I, [_P, _P, _P, _P]),
     "wharf_get_stats": (_I, [_P, _P]),
+    "wharf_export_index_paired": (_I, [_P, _P, _P]),
     "wharf_memory_footprint": (_I, [_P, _P]),
     "wharf_generate_batch_of_edges": (_I, [_I, _U64, _U64, _U64, _I, _I, C.c_double, C.c_double, C.c_double, _P, _P]),
     "wharf_szudzik64": (_I, [_I, _I, _U64, _P, _P, _P]),

@@ -5,6 +5,7 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
 #include <rocprim/device/device_select.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
@@ -954,6 +955,65 @@ int wharf_export_index(wharf_handle* h, uint64_t* counts, uint64_t* keys, uint32
             HIPCHK(hipMemcpyAsync(nexts, h->pairs.p, E * 4, hipMemcpyDeviceToHost, h->s));
         }
         HIPCHK(hipMemcpyAsync(counts, h->runs.p, h->n * 8, hipMemcpyDeviceToHost, h->s));
+        h->sync();
+    });
+}
+
+int wharf_export_index_paired(wharf_handle* h, uint64_t* counts, uint64_t* paired)
+{
+    return guarded(h, [&] {
+        REQUIRE(h && counts, WHARF_E_INVALID, "null argument");
+        int kb = 0;
+        const uint64_t E = build_index(h, kb);
+        const uint64_t n = h->n;
+        h->runs.ensure(n * 8);
+        HIPCHK(hipMemsetAsync(h->runs.p, 0, n * 8, h->s));
+        if (E) {
+            REQUIRE(paired, WHARF_E_INVALID, "null argument");
+            uint64_t* keys = h->k1.as<uint64_t>();
+            uint64_t* z = h->k2.as<uint64_t>();
+            launch_index_split(h->k2.as<uint64_t>(), E, kb, h->runs.as<unsigned long long>(), keys, h->s);
+            launch_index_pair(keys, h->pairs.as<uint32_t>(), E, z, h->s);
+            // per-vertex offsets, then each vertex's entries ascending (the C-tree
+            // iteration order), in chunks of < 2^31 entries for rocPRIM's 32-bit sizes
+            h->sel.ensure((n + 1) * 8);
+            uint64_t* off = h->sel.as<uint64_t>();
+            h->count.ensure((n + 1) * 8);
+            uint64_t* cnt = h->count.as<uint64_t>();
+            HIPCHK(hipMemcpyAsync(cnt, h->runs.p, n * 8, hipMemcpyDeviceToDevice, h->s));
+            HIPCHK(hipMemsetAsync(cnt + n, 0, 8, h->s));
+            h->rp([&](void* t, size_t& b) {
+                return rocprim::exclusive_scan(t, b, cnt, off, (uint64_t)0, (size_t)(n + 1), rocprim::plus<uint64_t>(), h->s);
+            });
+            std::vector<uint64_t> hoff(n + 1);
+            HIPCHK(hipMemcpyAsync(hoff.data(), off, (n + 1) * 8, hipMemcpyDeviceToHost, h->s));
+            h->sync();
+            const uint64_t kChunk = 1ull << 30;
+            h->flags.ensure((n + 1) * 4);
+            uint32_t* rel = h->flags.as<uint32_t>();
+            for (uint64_t v0 = 0; v0 < n;) {
+                uint64_t v1 = v0 + 1;   // at least one vertex per chunk
+                uint64_t lo = v0 + 1, hi = n;
+                while (lo <= hi) {   // largest v1 with hoff[v1] - hoff[v0] <= kChunk
+                    const uint64_t mid = lo + (hi - lo) / 2;
+                    if (hoff[mid] - hoff[v0] <= kChunk) { v1 = mid; lo = mid + 1; } else { hi = mid - 1; }
+                }
+                const uint64_t base = hoff[v0], size = hoff[v1] - base, segs = v1 - v0;
+                REQUIRE(size < (1ull << 32), WHARF_E_INVALID, "a vertex holds >= 2^32 index entries");
+                if (size) {
+                    launch_rel_offsets(off, v0, segs, rel, h->s);
+                    uint64_t* kin = z + base;
+                    uint64_t* kout = keys + base;
+                    h->rp([&](void* t, size_t& b) {
+                        return rocprim::segmented_radix_sort_keys(t, b, kin, kout, (unsigned)size, (unsigned)segs, rel,
+                                                                  rel + 1, 0u, 64u, h->s);
+                    });
+                }
+                v0 = v1;
+            }
+            HIPCHK(hipMemcpyAsync(paired, keys, E * 8, hipMemcpyDeviceToHost, h->s));
+        }
+        HIPCHK(hipMemcpyAsync(counts, h->runs.p, n * 8, hipMemcpyDeviceToHost, h->s));
         h->sync();
     });
 }

@@ -113,6 +113,8 @@ unsigned aff_blocks(uint64_t W);
 void launch_aff_count(const uint8_t* aff, uint64_t W, uint32_t* counts, hipStream_t s);
 void launch_aff_write(const uint8_t* aff, uint64_t W, const uint32_t* offs, uint64_t n, uint64_t n_loc, uint64_t lo,
                       uint32_t* out, hipStream_t s);
+void launch_index_pair(const uint64_t* keys, const uint32_t* nexts, uint64_t E, uint64_t* out, hipStream_t s);
+void launch_rel_offsets(const uint64_t* off, uint64_t v0, uint64_t cnt, uint32_t* rel, hipStream_t s);
 void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s);
 void launch_fill_u64(uint64_t* p, uint64_t cnt, uint64_t v, hipStream_t s);
 void launch_edge_hash_update(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, int insert, uint64_t* table,

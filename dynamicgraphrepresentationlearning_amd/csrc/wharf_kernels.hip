@@ -1419,6 +1419,28 @@ __global__ void k_szudzik64(int op, uint64_t cnt, uint64_t* __restrict__ x, uint
     }
 }
 
+// CompressedWalks entries (walks/compressed_walks.h:49-66): Szudzik(wid*L+pos, next)
+__global__ void k_index_pair(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ nexts, uint64_t E,
+                             uint64_t* __restrict__ out)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = keys[i], b = nexts[i];
+        out[i] = b >= a ? b * (b + 1) + a : a * a + b;
+    }
+}
+
+// offsets of vertices [v0, v0 + cnt] relative to off[v0] (segmented-sort chunk)
+__global__ void k_rel_offsets(const uint64_t* __restrict__ off, uint64_t v0, uint64_t cnt, uint32_t* __restrict__ rel)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= cnt; i += (uint64_t)gridDim.x * blockDim.x)
+        rel[i] = (uint32_t)(off[v0 + i] - off[v0]);
+}
+
+void launch_index_pair(const uint64_t* keys, const uint32_t* nexts, uint64_t E, uint64_t* out, hipStream_t s)
+{ if (E) hipLaunchKernelGGL(k_index_pair, grid_for(E, 256), 256, 0, s, keys, nexts, E, out); }
+void launch_rel_offsets(const uint64_t* off, uint64_t v0, uint64_t cnt, uint32_t* rel, hipStream_t s)
+{ hipLaunchKernelGGL(k_rel_offsets, grid_for(cnt + 1, 256), 256, 0, s, off, v0, cnt, rel); }
+
 unsigned grid_for(uint64_t work, unsigned block)
 {
     const uint64_t g = (work + block - 1) / block;

@@ -278,6 +278,17 @@ class WharfMH:
         L.check(L.lib.wharf_export_index(self._h, _ptr(counts), _ptr(keys), _ptr(nexts)), self._h, "export_index")
         return counts, keys[: sz.value], nexts[: sz.value]
 
+    def compressed_walks(self):
+        """The pairing-encoded CompressedWalks form (walks/compressed_walks.h:49-66):
+        per vertex, Szudzik(wid*L + pos, next) of its stored positions, ascending,
+        as 64-bit values.  Returns (counts[n], paired)."""
+        sz = C.c_uint64()
+        L.check(L.lib.wharf_index_size(self._h, C.byref(sz)), self._h, "index_size")
+        counts = np.zeros(self.number_of_vertices(), dtype=np.uint64)
+        paired = np.zeros(max(sz.value, 1), dtype=np.uint64)
+        L.check(L.lib.wharf_export_index_paired(self._h, _ptr(counts), _ptr(paired)), self._h, "export_index_paired")
+        return counts, paired[: sz.value]
+
 
 def generate_batch_of_edges(edges_number: int, vertices_number: int, batch_seed: int, self_loops: bool = False,
                             directed: bool = True, a: float = 0.5, b: float = 0.2, c: float = 0.1,

@@ -162,6 +162,14 @@ int wharf_walk_ids(wharf_handle* h, uint32_t* ids_out);
 int wharf_index_size(wharf_handle* h, uint64_t* size);
 int wharf_export_index(wharf_handle* h, uint64_t* counts, uint64_t* keys, uint32_t* nexts);
 
+/* The walks in the reference's pairing-encoded CompressedWalks form
+ * (walks/compressed_walks.h:49-66, pairings.h): per vertex, the values
+ * Szudzik(wid*L + pos, next) of its stored positions, ascending (the C-tree's
+ * iteration order), in 64 bits (the reference's 32-bit Szudzik<Vertex> would
+ * overflow past 2^16 keys).  counts[n] as for wharf_export_index; paired
+ * receives wharf_index_size() values. */
+int wharf_export_index_paired(wharf_handle* h, uint64_t* counts, uint64_t* paired);
+
 int wharf_get_stats(const wharf_handle* h, wharf_stats* out);
 
 /* WharfMH::memory_footprint (wharfmh.h:928-998), which prints the bytes of the

@@ -70,6 +70,35 @@ def test_six_vertex_golden(W, meta):
         g.destroy()
 
 
+def _paired_reference(counts, keys, nexts):
+    """CompressedWalks values from the golden (key, next) lists: per vertex,
+    Szudzik(key, next) ascending (the oracle's codec pins the formula)."""
+    a, b = keys.astype(np.uint64), nexts.astype(np.uint64)
+    z = np.where(b >= a, b * (b + np.uint64(1)) + a, a * a + b)
+    for i in range(0, len(z), max(len(z) // 17, 1)):
+        assert int(z[i]) == O.szudzik64_pair(int(a[i]), int(b[i]))
+    off = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+    return np.concatenate([np.sort(z[off[v]:off[v + 1]]) for v in range(len(counts))])
+
+
+def test_compressed_walks_pairing_export(W):
+    """wharf_export_index_paired against the golden inverted indexes."""
+    z = np.load(os.path.join(G, "six.npz"))
+    g = W.WharfMH.from_csr(z["off"], z["adj"], config=det_cfg(W, 2, 5))
+    g.generate_initial_random_walks()
+    c, p = g.compressed_walks()
+    np.testing.assert_array_equal(c, z["index_counts"])
+    np.testing.assert_array_equal(p, _paired_reference(z["index_counts"], z["index_keys"], z["index_nexts"]))
+    g.destroy()
+    r = np.load(os.path.join(G, "rmat10.npz"))
+    g = W.WharfMH.from_rmat(1024, 12800, 2048, seed=1, config=det_cfg(W, 2, 20))
+    g.generate_initial_random_walks()
+    c, p = g.compressed_walks()
+    np.testing.assert_array_equal(c, r["index_counts_0"])
+    np.testing.assert_array_equal(p, _paired_reference(r["index_counts_0"], r["index_keys_0"], r["index_nexts_0"]))
+    g.destroy()
+
+
 def test_rmat_batches_golden(W):
     z = np.load(os.path.join(G, "rmat_batches.npz"))
     for k in z.files:
