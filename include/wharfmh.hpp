@@ -145,6 +145,17 @@ public:
         check(wharf_export_index(h_, counts.data(), keys.data(), nexts.data()), h_, "export_index");
     }
 
+    // the pairing-encoded CompressedWalks form (walks/compressed_walks.h): per vertex,
+    // Szudzik(wid * L + pos, next) ascending, 64-bit
+    void compressed_walks(std::vector<uint64_t>& counts, std::vector<uint64_t>& paired)
+    {
+        uint64_t sz = 0;
+        check(wharf_index_size(h_, &sz), h_, "index_size");
+        counts.resize(number_of_vertices());
+        paired.resize(sz);
+        check(wharf_export_index_paired(h_, counts.data(), paired.data()), h_, "export_index_paired");
+    }
+
     // destroy / destroy_index (wharfmh.h:228, 237)
     void destroy()
     {

@@ -103,6 +103,22 @@ static void test_destroy(const Csr& g)
     std::vector<uint32_t> nx;
     w.inverted_index(c, k, nx);
     EXPECT(!k.empty());
+    std::vector<uint64_t> pc, paired;   // CompressedWalks form: same counts, Szudzik(key, next) per entry
+    w.compressed_walks(pc, paired);
+    EXPECT(pc == c && paired.size() == k.size());
+    {
+        bool same = true;
+        for (size_t v = 0, o = 0; v < c.size() && same; o += c[v], v++) {
+            std::vector<uint64_t> z;
+            for (uint64_t i = o; i < o + c[v]; i++) {
+                const uint64_t a = k[i], b = nx[i];
+                z.push_back(b >= a ? b * (b + 1) + a : a * a + b);
+            }
+            std::sort(z.begin(), z.end());
+            same = std::equal(z.begin(), z.end(), paired.begin() + o);
+        }
+        EXPECT(same);
+    }
     const wharf_memory mem = w.memory_footprint();   // memory-footprint.cpp's report
     EXPECT(mem.n == g.n && mem.m == g.m && mem.walks_bytes >= k.size() * 4 && mem.csr_bytes >= g.m * 4);
     EXPECT(mem.total_bytes >= mem.csr_bytes + mem.records_bytes + mem.walks_bytes);
