@@ -197,9 +197,11 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
+    warm_ms = []
     for i in range(args.warmup):
         g.generate_initial_random_walks()
-        log(f"[rank {rank}] warmup {i}: {g.stats()['last_walk_kernel_ms']:.1f} ms")
+        warm_ms.append(g.stats()["last_walk_kernel_ms"])
+        log(f"[rank {rank}] warmup {i}: {warm_ms[-1]:.1f} ms")
     barrier()
     t_start = time.perf_counter()
     kern_ms = []
@@ -329,6 +331,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
                          "traffic": traffic, "bytes_per_step": bytes_per_step,
                          "avg_kernel_ms": round(avg_kernel_ms, 3),
+                         # the first generation of a fresh handle (node2vec: every anchor initialised)
+                         "first_generation_kernel_ms": round(warm_ms[0], 3) if warm_ms else None,
                          "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3), live_ceiling)
                          if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None},
             "rewalk_latency_10k_batch": rewalk,
