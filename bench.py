@@ -305,6 +305,9 @@ def main():
 
     if rank == 0:
         live_ceiling = measure_gather_ceiling() if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None
+        if rewalk and live_ceiling:
+            # re-walk steps (one gather each) against the same ceiling; the scan rides along
+            rewalk["rewalk_frac_of_gather_ceiling"] = round(rewalk["rewalk_Gsteps_per_s"] / live_ceiling, 4)
         achieved = (steps_local * bytes_per_step / (avg_kernel_ms * 1e-3) / 1e9) if bytes_per_step else None
         traffic = load_traffic(tag)
         line = {
