@@ -220,6 +220,29 @@ def test_edge_cases_isolated_dead_ends_and_flags(W):
     _compare_stream(W, off, adj, batches, wpv=2, L=9, model=0, deterministic=False, seed=9)
 
 
+@pytest.mark.parametrize("wpv,L", [(3, 2), (1, 255), (255, 7)])
+@pytest.mark.parametrize("mode", ["det", "deepwalk", "node2vec"])
+def test_extreme_walk_shapes(W, wpv, L, mode):
+    """The u8 limits of types::Position / walks_per_vertex (L = 2 and 255, wpv = 255)
+    through generation and updates, against the oracle."""
+    base = O.generate_batch_of_edges(3000, 512, 8, False, False)
+    off, adj = O.csr_from_edges(300, base)
+    batches = [(True, O.generate_batch_of_edges(200, 300, 21, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
+               (False, O.generate_batch_of_edges(150, 300, 22, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES)]
+    kw = dict(deterministic=True) if mode == "det" else dict(
+        deterministic=False, seed=5, model=1 if mode == "node2vec" else 0, paramP=0.5, paramQ=2.0)
+    _compare_stream(W, off, adj, batches, wpv=wpv, L=L, **kw)
+
+
+def test_single_vertex_graph(W):
+    g = W.WharfMH(1, 0, config=det_cfg(W, 3, 4))
+    g.generate_initial_random_walks()
+    assert (g.walks()[:, 0] == 0).all() and (g.walks()[:, 1:] == W.SENTINEL).all()
+    aff = g.insert_edges_batch(np.array([[0, 0]], np.uint32))     # a self loop: every walk re-walks on it
+    assert aff.tolist() == [0, 1, 2] and (g.walks() == 0).all()
+    g.destroy()
+
+
 def test_empty_graph_and_errors(W):
     g = W.WharfMH(10, 0, config=det_cfg(W, 2, 5))
     assert g.number_of_edges() == 0
