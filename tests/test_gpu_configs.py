@@ -97,3 +97,16 @@ def test_config4_node2vec_mixed_8_shards(W):
         batches += [(True, e), (False, e)]
     _sharded_stream(W, n, off, adj, dict(walks_per_vertex=4, walk_length=40, model=1, paramP=0.5, paramQ=2.0,
                                          deterministic=False, seed=77), batches, 8)
+
+
+def test_node2vec_long_mixed_stream_vs_oracle(W):
+    """25 batches of mixed inserts/deletes (undirected and directed) on one
+    handle: the anchor cache's epoch tags stay exact across many resets."""
+    n, off, adj = _graph(11, 25000, 9)
+    rng = np.random.default_rng(3)
+    batches = []
+    for b in range(25):
+        e = O.generate_batch_of_edges(int(rng.integers(20, 400)), n, 100 + b, False, bool(b % 3 == 2))
+        batches.append((bool(rng.integers(0, 2)) or b < 3, e, O.REMOVE_DUPS | O.APPLY_WALK_UPDATES))
+    from test_gpu_parity import _compare_stream
+    _compare_stream(W, off, adj, batches, wpv=3, L=30, model=1, paramP=0.5, paramQ=2.0, deterministic=False, seed=41)
