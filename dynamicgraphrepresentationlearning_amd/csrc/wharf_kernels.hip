@@ -232,9 +232,21 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
             const uint32_t ai = anchor_get(a, w.rc, w.rp, w.ein, w.anc, acls);
             bool ok = true;   // proposing the anchor itself is always accepted
             if (ai != ci) {
-                const float wc = weight<MODEL>(a, w.rp, cand.v);
+                // metropolis_hastings_sampler.h:118-122: accept iff w(a) < w(c) or
+                // u <= w(c) / w(a).  A non-return candidate weighs 1 (triangle) or
+                // 1/q (outward); when both weights give the same decision the
+                // class, and so the has_edge probe, cannot matter (on sparse-
+                // triangle graphs the anchor is mostly outward, and an outward
+                // anchor accepts every candidate).
                 const float wa = class_weight(a, acls);
-                ok = (wa < wc) || (u01(q.x1, q.x2) <= (double)wc / (double)wa);
+                const double u = u01(q.x1, q.x2);
+                auto accept = [&](float wc) { return (wa < wc) || (u <= (double)wc / (double)wa); };
+                if (cand.v == w.rp.v) {
+                    ok = accept(a.inv_p);
+                } else {
+                    const bool ok_tri = accept(1.0f), ok_out = accept(a.inv_q);
+                    ok = ok_tri == ok_out ? ok_tri : (has_edge(a, w.rp, cand.v) ? ok_tri : ok_out);
+                }
             }
             accepts += ok;
             w.ein = (int64_t)(w.rc.off + (ok ? ci : ai));
