@@ -139,16 +139,29 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
     }
     P4 r = philox4x32_10(rc.v, rp.v, 0, ep | kStreamAnchor, a.key0, a.key1);
     uint32_t last = (uint32_t)pick32(r.x0, rc.deg);
+    uint32_t lcls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + last]);
     if (a.init == kInitBurnin) {
+        // 100 MH moves (metropolis_hastings_sampler.h:96-104); the current
+        // anchor's class is carried instead of re-probed, and a candidate's
+        // has_edge is skipped when it is rejected whatever its class
         for (uint32_t i = 0; i < 100; i++) {
             r = philox4x32_10(rc.v, rp.v, i, ep | kStreamBurnin, a.key0, a.key1);
             const uint32_t cand = (uint32_t)pick32(r.x0, rc.deg);
-            const float wn = weight<kNode2Vec>(a, rp, a.adj[rc.off + cand]);
-            const float wl = weight<kNode2Vec>(a, rp, a.adj[rc.off + last]);
-            if (wl < wn || u01(r.x1, r.x2) <= (double)wn / (double)wl) last = cand;
+            const uint32_t cv = a.adj[rc.off + cand];
+            const float wl = class_weight(a, lcls);
+            const double u = u01(r.x1, r.x2);
+            auto move = [&](float wn) { return (wl < wn) || (u <= (double)wn / (double)wl); };
+            if (cv == rp.v) {
+                if (move(a.inv_p)) { last = cand; lcls = 0; }
+                continue;
+            }
+            const bool m_tri = move(1.0f), m_out = move(a.inv_q);
+            if (!m_tri && !m_out) continue;   // rejected whatever the class
+            const uint32_t c = has_edge(a, rp, cv) ? 1u : 2u;
+            if (c == 1 ? m_tri : m_out) { last = cand; lcls = c; }
         }
     }
-    cls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + last]);
+    cls = lcls;
     return last;
 }
 
