@@ -338,6 +338,7 @@ def main():
                          "first_generation_kernel_ms": round(warm_ms[0], 3) if warm_ms else None,
                          "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3), live_ceiling)
                          if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None},
+            "mh_accept_rate": round(st["accepts"] / st["steps"], 5) if st["steps"] else None,
             "rewalk_latency_10k_batch": rewalk,
             "corpus_allgatherv": corpus,
             "cpu_baseline": None,

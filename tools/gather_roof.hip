@@ -45,9 +45,10 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ t, uin
                                                 uint64_t W, int L)
 {
     const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (li >= W) return;
+    if (li >= W) return;   // W is a multiple of 256: whole blocks (modes 11/12 synchronise)
     uint32_t x = mix((uint32_t)li);
     uint32_t b0 = 0, b1 = 0, b2 = 0;   // mode 8: 4-step store buffer
+    __shared__ uint32_t tile[16 * 256];   // modes 11/12: 16 steps x 256 lanes staged in LDS
     for (int p = 0; p < L; p++) {
         uint64_t slot;
         if (MODE == 4) {                                                          // dep + Philox4x32-10 per step
@@ -91,6 +92,24 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ t, uin
             out[li] = r.x;
         } else if (MODE == 10) {  // dep, non-temporal store
             __builtin_nontemporal_store(r.x, out + (uint64_t)p * W + li);
+        } else if (MODE == 11 || MODE == 12) {   // dep, 16 steps staged in LDS, then one burst per block
+            tile[(p & 15) * 256 + threadIdx.x] = r.x;
+            if ((p & 15) == 15 || p == L - 1) {
+                __syncthreads();
+                const int rows = (p & 15) + 1, p0 = p & ~15;
+                if (MODE == 11) {   // [p/16][W][16]: the block's 16 KB chunk is contiguous
+                    uint4* o = reinterpret_cast<uint4*>(out + (uint64_t)p0 * W + (uint64_t)blockIdx.x * 256 * 16);
+                    for (int k = threadIdx.x; k < 256 * 4; k += 256) {
+                        const int lane = k >> 2, q = (k & 3) * 4;
+                        o[k] = make_uint4(tile[q * 256 + lane], tile[(q + 1) * 256 + lane], tile[(q + 2) * 256 + lane],
+                                          tile[(q + 3) * 256 + lane]);
+                    }
+                } else {            // position-major as the walk matrix, written 16 rows at once
+                    for (int k = 0; k < rows; k++)
+                        out[(uint64_t)(p0 + k) * W + (uint64_t)blockIdx.x * 256 + threadIdx.x] = tile[k * 256 + threadIdx.x];
+                }
+                __syncthreads();
+            }
         } else if (MODE != 7 || r.x == 0xFFFFFFFFu) {
             out[(uint64_t)p * W + li] = r.x;   // 7: dep without the store
         }
@@ -111,16 +130,17 @@ int main(int argc, char** argv)
     if (!std::strcmp(kind, "uncached")) CHK(hipExtMallocWithFlags((void**)&t, n * 16, hipDeviceMallocUncached));
     else if (!std::strcmp(kind, "fine")) CHK(hipExtMallocWithFlags((void**)&t, n * 16, hipDeviceMallocFinegrained));
     else CHK(hipMalloc(&t, n * 16));
-    CHK(hipMalloc(&out, W * L * 4));
+    CHK(hipMalloc(&out, W * ((L + 15) / 16 * 16) * 4));   // mode 11 writes whole 16-step chunks
     hipLaunchKernelGGL(k_init, 4096, 256, 0, 0, t, n);
     CHK(hipDeviceSynchronize());
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
-    const char* names[11] = {"dep", "indep", "stream", "dep_nt", "dep_philox", "dep_4B", "dep_8B", "dep_nostore",
-                             "dep_store16B_per_4", "dep_store_same_row", "dep_store_nt"};
+    const char* names[13] = {"dep", "indep", "stream", "dep_nt", "dep_philox", "dep_4B", "dep_8B", "dep_nostore",
+                             "dep_store16B_per_4", "dep_store_same_row", "dep_store_nt",
+                             "dep_store_lds16_tiled", "dep_store_lds16_rows"};
     for (int rep = 0; rep < 2; rep++)
-        for (int mode = 0; mode < 11; mode++) {
+        for (int mode = 0; mode < 13; mode++) {
             if (only && std::strcmp(only, names[mode]) != 0) continue;
             CHK(hipEventRecord(a));
             if (mode == 0) hipLaunchKernelGGL(k_gather<0>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
@@ -134,6 +154,8 @@ int main(int argc, char** argv)
             if (mode == 8) hipLaunchKernelGGL(k_gather<8>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 9) hipLaunchKernelGGL(k_gather<9>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 10) hipLaunchKernelGGL(k_gather<10>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 11) hipLaunchKernelGGL(k_gather<11>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 12) hipLaunchKernelGGL(k_gather<12>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             CHK(hipEventRecord(b));
             CHK(hipEventSynchronize(b));
             float ms;

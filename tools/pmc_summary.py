@@ -21,12 +21,20 @@ import statistics
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_launch(path, kernel, counter):
+def per_launch(path, kernel, counter, skip=0):
     vals = []
     for r in csv.DictReader(open(path)):
         if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
             vals.append(float(r["Counter_Value"]))
-    return vals
+    return vals[skip:]
+
+
+def trace_avg_ns(path, kernel, skip=0):
+    """average duration from a --kernel-trace csv, dispatch order, first `skip` launches dropped"""
+    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[skip:]]
+    return statistics.mean(d) if d else None
 
 
 def main():
@@ -35,22 +43,28 @@ def main():
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
-    ap.add_argument("--stats", required=True)
+    ap.add_argument("--stats", default=None, help="rocprofv3 --stats kernel_stats.csv")
+    ap.add_argument("--trace", default=None, help="rocprofv3 --kernel-trace kernel_trace.csv (with --skip)")
+    ap.add_argument("--skip", type=int, default=0,
+                    help="drop the first launches (node2vec: the first generation also initialises every anchor)")
     ap.add_argument("--round", default="r01")
     ap.add_argument("--algorithmic-bytes", type=float, default=None)
     a = ap.parse_args()
-    f = per_launch(a.fetch, a.kernel, "FETCH_SIZE")
-    w = per_launch(a.write, a.kernel, "WRITE_SIZE")
+    f = per_launch(a.fetch, a.kernel, "FETCH_SIZE", a.skip)
+    w = per_launch(a.write, a.kernel, "WRITE_SIZE", a.skip)
     avg_ns = None
-    for r in csv.DictReader(open(a.stats)):
-        if a.kernel in r["Name"]:
-            avg_ns = float(r["AverageNs"])
-            break
+    if a.trace:
+        avg_ns = trace_avg_ns(a.trace, a.kernel, a.skip)
+    else:
+        for r in csv.DictReader(open(a.stats)):
+            if a.kernel in r["Name"]:
+                avg_ns = float(r["AverageNs"])
+                break
     fetch_raw = statistics.mean(f) * 1024
     write = statistics.mean(w) * 1024
     out = {
         "kernel": a.kernel,
-        "launches": {"fetch_pass": len(f), "write_pass": len(w)},
+        "launches": {"fetch_pass": len(f), "write_pass": len(w), "skipped_first": a.skip},
         "fetch_size_bytes_raw": fetch_raw,
         "fetch_bytes_corrected": 2 * fetch_raw,
         "write_bytes": write,
@@ -58,7 +72,7 @@ def main():
         "avg_kernel_ns_kernel_trace": avg_ns,
         "effective_GBps": (2 * fetch_raw + write) / avg_ns if avg_ns else None,
         "algorithmic_bytes_per_launch": a.algorithmic_bytes,
-        "sources": [os.path.relpath(p, REPO) for p in (a.fetch, a.write, a.stats)],
+        "sources": [os.path.relpath(p, REPO) for p in (a.fetch, a.write, a.trace or a.stats)],
     }
     dst = os.path.join(REPO, "profiles", f"pmc_{a.tag}.json")
     json.dump(out, open(dst, "w"), indent=1)
