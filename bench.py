@@ -11,6 +11,13 @@ the replicated CSR and owns a contiguous start-vertex range of the walks
 
 A "step" = one generate_initial_random_walks() over the whole graph (all
 ranks' shards).  value = transitions appended by all ranks per second.
+
+Scaling (--scaling, default weak): every rank keeps the configs[1] per-GPU
+workload (4.19 M start vertices x 10 walks x 80): at N ranks the replicated RMAT
+graph has scale 22 + log2 N and N x 117 M undirected samples (N = 8: scale 25,
+~1.9 G CSR entries, the configs[3] twitter size), and rank g walks from its own
+start-vertex range.  --scaling strong keeps the scale-22 graph and splits its
+walks N ways.
 """
 from __future__ import annotations
 
@@ -58,6 +65,9 @@ def parse():
     p.add_argument("--cpu-baseline", choices=["auto", "reference", "port", "off"], default="auto")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-timeout", type=int, default=300)
+    p.add_argument("--cpu-length", type=int, default=24,
+                   help="walk length of the bounded reference CPU sample (~15-25 s on 16 host threads)")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     return p.parse_args()
 
 
@@ -119,12 +129,13 @@ def cpu_cores(requested: int) -> int:
 
 def cpu_baseline(args, n, active_vertices, off, adj, kind):
     """Reference CPU path (oracle/_ref/ref_harness, the reference's own headers)
-    on a bounded sample: the same RMAT graph, 1 walk per vertex (1/10 of the
-    workload's walks), same length and model, MH mode, timed generate only."""
+    on a bounded sample: the same RMAT graph and model, MH mode, 1 walk per
+    vertex (1/10 of the workload's walks) of length --cpu-length (24 instead
+    of 80, so the sample is ~15-25 s of CPU work), timed generate only."""
     cores = cpu_cores(args.cpu_threads)
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
     if kind in ("auto", "reference") and os.path.exists(harness):
-        cmd = [harness, "cfg", "1", str(args.length), args.model, str(args.paramP), str(args.paramQ), "weight",
+        cmd = [harness, "cfg", "1", str(args.cpu_length), args.model, str(args.paramP), str(args.paramQ), "weight",
                "1" if args.det else "0", "42",
                "graph-rmat", str(args.samples), str(2 * n), str(args.seed), str(n), "time-gen", "1"]
         env = dict(os.environ, NUM_THREADS=str(cores))
@@ -134,10 +145,11 @@ def cpu_baseline(args, n, active_vertices, off, adj, kind):
             m = re.search(r"time-gen seconds=([0-9.]+)", r.stdout)
             if r.returncode == 0 and m:
                 secs = float(m.group(1))
-                steps = active_vertices * (args.length - 1)
+                steps = active_vertices * (args.cpu_length - 1)
                 return {"value": steps / secs, "unit": "walk-steps/s", "cores": cores, "kind": "reference",
                         "sample": f"reference WharfMH::generate_initial_random_walks on the same RMAT graph "
-                                  f"(n={n}), walks_per_vertex=1 (1/{args.wpv} of the workload), L={args.length}, "
+                                  f"(n={n}), walks_per_vertex=1 (1/{args.wpv} of the workload), L={args.cpu_length} "
+                                  f"(workload: {args.length}), "
                                   f"{'deterministic' if args.det else 'MH'} {args.model}; {steps} steps in {secs:.2f} s",
                         "seconds": secs}
             log("cpu_baseline: harness failed", r.returncode, r.stderr[-500:])
@@ -178,15 +190,20 @@ def main():
             dist.init_process_group(backend)
     import dynamicgraphrepresentationlearning_amd as W
 
-    n = 1 << args.scale
+    # weak scaling: the replicated graph grows with the ranks so each rank keeps
+    # configs[1]'s per-GPU walk count (N = 2^k ranks: scale + k, samples x N)
+    grow = (max(world, 1) - 1).bit_length() if args.scaling == "weak" else 0
+    scale = args.scale + grow
+    samples = args.samples * (1 << grow)
+    n = 1 << scale
     cfg = W.WharfConfig(walks_per_vertex=args.wpv, walk_length=args.length,
                         model=W.NODE2VEC if args.model == "node2vec" else W.DEEPWALK,
                         paramP=args.paramP, paramQ=args.paramQ, deterministic=args.det, seed=0x5EED)
     t0 = time.time()
-    g = W.WharfMH.from_rmat(n, args.samples, 2 * n, seed=args.seed, config=cfg, device=dev)
-    off, adj = g.flatten_graph() if rank == 0 else (None, None)
-    off_np = off if off is not None else g.flatten_graph()[0]
-    deg = np.diff(off_np.astype(np.int64))
+    g = W.WharfMH.from_rmat(n, samples, 2 * n, seed=args.seed, config=cfg, device=dev)
+    # the whole CSR on the host only where the CPU baseline may need it (N = 1)
+    off, adj = g.flatten_graph() if world == 1 else (g.offsets(), None)
+    deg = np.diff(off.astype(np.int64))
     lo, hi = balanced_shards(deg, world)[rank]
     g.set_shard(lo, hi)
     m = g.number_of_edges()
@@ -223,7 +240,7 @@ def main():
     value = steps_total * args.steps / t_max
     avg_kernel_ms = float(np.mean(kern_ms))
     bytes_per_step = BYTES_PER_STEP_DEEPWALK if args.model == "deepwalk" or args.det else BYTES_PER_STEP_NODE2VEC
-    tag = f"gen_{args.model}_{'det' if args.det else 'mh'}_s{args.scale}"
+    tag = f"gen_{args.model}_{'det' if args.det else 'mh'}_s{scale}"
 
     # corpus reassembly for the downstream consumer: full-mesh all-gatherv over RCCL (not timed in `value`)
     corpus = None
@@ -232,14 +249,17 @@ def main():
         shards = balanced_shards(deg, world)
         loc = torch.empty((g.number_of_walks, args.length), dtype=torch.int32, device=f"cuda:{dev}")
         g.export_walks_device(loc.data_ptr(), layout="walk")
-        loc = loc.to(comm_dev)
+        # the whole corpus on every rank, or its first rounds when it would not fit
+        # beside the graph (weak scaling at N = 8: a 107 GB corpus); local rows are round-major
+        rounds = max(1, min(args.wpv, (16 << 30) // max(n * args.length * 4, 1)))
+        loc = loc[: (hi - lo) * rounds].to(comm_dev)
         barrier()
         t1 = time.perf_counter()
-        full = allgatherv_corpus(loc, shards, n, args.wpv)
+        full = allgatherv_corpus(loc, shards, n, rounds)
         barrier()
         gms = (time.perf_counter() - t1) * 1e3
         recv = full.numel() * 4 - loc.numel() * 4
-        corpus = {"ms": round(gms, 3), "bytes_received_per_rank": int(recv),
+        corpus = {"ms": round(gms, 3), "rounds": rounds, "bytes_received_per_rank": int(recv),
                   "GBps_per_rank": round(recv / gms / 1e6, 1), "pattern": "batch_isend_irecv full mesh"}
         del full, loc
 
@@ -249,9 +269,9 @@ def main():
     # (memory-throughput-latency.cpp:126-134: generate_batch_of_edges(5000, n, seed=b, false, undirected))
     rewalk = None
     if args.rewalk_batches > 0:
-        gs = W.WharfMH.from_rmat(n, args.stream_samples, 2 * n, seed=args.seed + 1, config=cfg, device=dev)
-        gs.set_shard(lo, hi) if world == 1 else gs.set_shard(*balanced_shards(
-            np.diff(gs.flatten_graph()[0].astype(np.int64)), world)[rank])
+        ns = 1 << args.scale   # configs[2] is a one-GPU graph: not grown with the ranks
+        gs = W.WharfMH.from_rmat(ns, args.stream_samples, 2 * ns, seed=args.seed + 1, config=cfg, device=dev)
+        gs.set_shard(*balanced_shards(np.diff(gs.offsets().astype(np.int64)), world)[rank])
         gs.generate_initial_random_walks()
         gs.generate_initial_random_walks()
         s1 = gs.stats()
@@ -261,7 +281,7 @@ def main():
         out = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
         lat, aff, gu, wu, kern, rsteps = [], [], [], [], [], []
         for b in range(args.rewalk_batches):
-            batch = W.generate_batch_of_edges(5000, n, b, False, False, device=dev)
+            batch = W.generate_batch_of_edges(5000, ns, b, False, False, device=dev)
             barrier()
             t1 = time.perf_counter()
             a = gs.insert_edges_batch(batch, remove_dups=True, out=out)
@@ -276,7 +296,7 @@ def main():
         hout = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, pin_memory=True).numpy().view(np.uint32)
         lat_host = []
         for b in range(args.rewalk_batches, args.rewalk_batches + min(5, args.rewalk_batches)):
-            batch = W.generate_batch_of_edges(5000, n, b, False, False, device=dev)
+            batch = W.generate_batch_of_edges(5000, ns, b, False, False, device=dev)
             barrier()
             t1 = time.perf_counter()
             gs.insert_edges_batch(batch, remove_dups=True, out=hout)
@@ -319,12 +339,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic RMAT (utility::generate_batch_of_edges semantics, a=.5 b=.2 c=.1), built on device",
-            "config": {"workload": f"configs[1] com-orkut-sized initial walk generation: RMAT scale {args.scale} "
-                                   f"(n={n}), {args.samples} undirected samples (seed {args.seed}) -> m={m} CSR "
+            "config": {"workload": f"configs[1] com-orkut-sized initial walk generation"
+                                   f"{' per GPU (weak scaling)' if grow else ''}: RMAT scale {scale} "
+                                   f"(n={n}), {samples} undirected samples (seed {args.seed}) -> m={m} CSR "
                                    f"entries; {args.model} {'deterministic' if args.det else 'MH'}, "
                                    f"walks_per_vertex={args.wpv}, walk_length={args.length}",
                        "n": n, "m": m, "walks": n * args.wpv, "transitions_per_step": steps_total,

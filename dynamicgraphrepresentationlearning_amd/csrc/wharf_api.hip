@@ -743,9 +743,9 @@ int wharf_set_shard(wharf_handle* h, uint64_t lo, uint64_t hi)
 int wharf_get_graph(wharf_handle* h, uint64_t* offsets_out, uint32_t* targets_out)
 {
     return guarded(h, [&] {
-        REQUIRE(h && offsets_out && (h->m == 0 || targets_out), WHARF_E_INVALID, "null argument");
+        REQUIRE(h && offsets_out, WHARF_E_INVALID, "null argument");
         HIPCHK(hipMemcpyAsync(offsets_out, h->off.p, (h->n + 1) * 8, hipMemcpyDeviceToHost, h->s));
-        if (h->m) HIPCHK(hipMemcpyAsync(targets_out, h->adj.p, h->m * 4, hipMemcpyDeviceToHost, h->s));
+        if (h->m && targets_out) HIPCHK(hipMemcpyAsync(targets_out, h->adj.p, h->m * 4, hipMemcpyDeviceToHost, h->s));
         h->sync();
     });
 }

@@ -23,6 +23,7 @@ Errors raise RuntimeError (the reference calls std::exit(1) / asserts).
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -73,7 +74,8 @@ class WharfMH:
 
     def __init__(self, n: int, m: int = 0, offsets=None, edges=None, config: WharfConfig | None = None,
                  device: int = 0, _handle=None):
-        self.config = config or WharfConfig()
+        # a copy: set_shard records the shard here, not in the caller's object
+        self.config = dataclasses.replace(config) if config is not None else WharfConfig()
         self._cfg = self.config.to_c()
         self.device = device
         if _handle is not None:
@@ -177,6 +179,12 @@ class WharfMH:
         adj = np.zeros(max(m, 1), dtype=np.uint32)
         L.check(L.lib.wharf_get_graph(self._h, _ptr(off), _ptr(adj)), self._h, "flatten_graph")
         return off, adj[:m]
+
+    def offsets(self) -> np.ndarray:
+        """CSR row offsets only (n + 1 u64; the targets stay on the device)."""
+        off = np.zeros(self.number_of_vertices() + 1, dtype=np.uint64)
+        L.check(L.lib.wharf_get_graph(self._h, _ptr(off), None), self._h, "offsets")
+        return off
 
     # -- the walk path ------------------------------------------------------------------------
     def generate_initial_random_walks(self) -> None:

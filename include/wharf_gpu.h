@@ -134,7 +134,8 @@ int wharf_shard(const wharf_handle* h, uint64_t* lo, uint64_t* hi, uint64_t* wal
  * [lo, hi) (hi == 0: all).  Drops the current walks (like destroy_index). */
 int wharf_set_shard(wharf_handle* h, uint64_t lo, uint64_t hi);
 
-/* flatten_graph (wharfmh.h:175-208): offsets_out n+1 entries, targets_out m. */
+/* flatten_graph (wharfmh.h:175-208): offsets_out n+1 entries, targets_out m
+ * (targets_out NULL: offsets only). */
 int wharf_get_graph(wharf_handle* h, uint64_t* offsets_out, uint32_t* targets_out);
 
 /* WharfMH::walk / vertex_at_walk (wharfmh.h:365-427).

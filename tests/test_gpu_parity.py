@@ -130,6 +130,7 @@ def test_rmat10_streaming_golden(W):
             o2, a2 = g.flatten_graph()
             np.testing.assert_array_equal(o2, z[f"off_{gtag}"], err_msg=tag)
             np.testing.assert_array_equal(a2, z[f"adj_{gtag}"], err_msg=tag)
+            np.testing.assert_array_equal(g.offsets(), o2, err_msg=tag)
             np.testing.assert_array_equal(g.walks(), z[f"walks_{wname}"], err_msg=tag)
             if f"index_counts_{gtag}" in z.files:
                 c, k, nx = g.inverted_index()
@@ -495,3 +496,17 @@ def test_shards_reproduce_the_full_corpus(W, mode):
             g.walk(int(np.setdiff1d(np.arange(3 * n), ids)[0]))   # not owned by this shard
         g.destroy()
     full.destroy()
+
+
+def test_set_shard_keeps_the_callers_config(W):
+    """set_shard re-partitions one handle; a config shared with a later handle on a
+    smaller graph (bench.py's stream graph) keeps its own shard fields."""
+    cfg = W.WharfConfig(walks_per_vertex=2, walk_length=10)
+    g = W.WharfMH.from_rmat(1 << 12, 30000, 1 << 13, seed=3, config=cfg)
+    g.set_shard(100, 1 << 12)
+    assert (cfg.shard_lo, cfg.shard_hi) == (0, 0)
+    assert g.shard()[:2] == (100, 1 << 12)
+    h = W.WharfMH.from_rmat(1 << 10, 5000, 1 << 11, seed=3, config=cfg)
+    assert h.shard()[:2] == (0, 1 << 10)
+    h.destroy()
+    g.destroy()
