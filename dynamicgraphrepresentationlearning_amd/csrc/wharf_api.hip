@@ -86,6 +86,8 @@ struct wharf_handle {
     uint32_t epoch = 0;
     DevBuf off, adj, vrec, erec, row_epoch, off2, adj2, anchor2, ehash, erec2;
     uint64_t ehash_mask = 0, ehash_used = 0;   // capacity - 1; occupied slots incl. tombstones
+    DevBuf fdir, fpool, fplan;                 // node2vec MH: per-row neighbour filters (k_filter_*)
+    uint64_t fpool_used = 0;                   // words handed out (rows that outgrew theirs leave gaps)
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
     DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, rtabs, count, pairs, sel, defer, esave;
     wharf_stats st{};
@@ -143,6 +145,7 @@ struct wharf_handle {
         HIPCHK(hipMemsetAsync(row_epoch.p, 0, std::max<uint64_t>(n, 1) * 4, s));
         build_records();
         if (anchors) build_edge_hash();
+        if (anchors) build_filters();
         bitmap.ensure((bitmap_words() + kBloomWords) * 4);   // exact bitmap, then the Bloom filter
         sync();
     }
@@ -181,6 +184,59 @@ struct wharf_handle {
         launch_edge_hash_build(off.as<uint64_t>(), n, adj.as<uint32_t>(), ehash.as<uint64_t>(), ehash_mask, s);
     }
 
+    // neighbour filters of every row: sizes, directory (exclusive scan), fill;
+    // the pool keeps 1/4 headroom for rows that outgrow their words in batches
+    void build_filters()
+    {
+        const char* off_env = getenv("WHARF_NO_NEIGHBOUR_FILTER");
+        if (off_env && atoi(off_env)) { fdir.release(); fpool.release(); return; }
+        DevBuf words;
+        words.ensure((n + 1) * 8);
+        fdir.ensure((n + 1) * 8);
+        launch_filter_sizes(off.as<uint64_t>(), n, words.as<uint64_t>(), s);
+        uint64_t* in = words.as<uint64_t>();
+        uint64_t* out = fdir.as<uint64_t>();
+        rp([&](void* t, size_t& b) {
+            return rocprim::exclusive_scan(t, b, in, out, (uint64_t)0, (size_t)(n + 1), rocprim::plus<uint64_t>(), s);
+        });
+        uint64_t total = 0;
+        HIPCHK(hipMemcpyAsync(&total, fdir.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+        sync();
+        words.release();
+        // WHARF_FILTER_NO_SLACK (tests): no headroom, so every row that outgrows its words re-builds all
+        const char* ns = getenv("WHARF_FILTER_NO_SLACK");
+        const uint64_t want = std::max<uint64_t>(ns && atoi(ns) ? total : total + total / 4, 1) * 8;
+        if (fpool.cap > want + want / 2) fpool.release();   // do not keep a much larger pool
+        fpool.ensure(want);
+        fpool_used = total;
+        HIPCHK(hipMemsetAsync(fpool.p, 0, total * 8, s));
+        launch_filter_pack(off.as<uint64_t>(), n, fdir.as<uint64_t>(), s);
+        launch_filter_fill(off.as<uint64_t>(), n, adj.as<uint32_t>(), fdir.as<uint64_t>(), fpool.as<uint64_t>(), s);
+    }
+
+    // after a batch: rebuild the filters of the k batch sources from their new rows
+    void update_filters(const RunInfo* runs_d, uint64_t k)
+    {
+        if (!fpool.p || !k) return;
+        fplan.ensure((k + 1) * 16);
+        uint64_t* need = fplan.as<uint64_t>();
+        uint64_t* gofs = need + k + 1;
+        launch_filter_plan(runs_d, k, off.as<uint64_t>(), fdir.as<uint64_t>(), need, s);
+        rp([&](void* t, size_t& b) {
+            return rocprim::exclusive_scan(t, b, need, gofs, (uint64_t)0, (size_t)(k + 1), rocprim::plus<uint64_t>(), s);
+        });
+        uint64_t grow = 0;
+        HIPCHK(hipMemcpyAsync(&grow, gofs + k, 8, hipMemcpyDeviceToHost, s));
+        sync();
+        if (fpool_used + grow > fpool.cap / 8) {
+            build_filters();   // out of headroom: re-size and re-fill every row (drops the gaps)
+            return;
+        }
+        launch_filter_rows(runs_d, k, off.as<uint64_t>(), adj.as<uint32_t>(), need, gofs, fpool_used,
+                           fdir.as<uint64_t>(), fpool.as<uint64_t>(), s);
+        fpool_used += grow;
+    }
+
     WalkArgs walk_args()
     {
         ensure_walks();
@@ -191,6 +247,8 @@ struct wharf_handle {
         a.anchor = anchors ? erec.as<uint64_t>() + 2 : nullptr;   // inside the 32-B records
         a.ehash = anchors ? ehash.as<uint64_t>() : nullptr;
         a.ehash_mask = ehash_mask;
+        a.fdir = anchors && fpool.p ? fdir.as<uint64_t>() : nullptr;
+        a.fpool = anchors && fpool.p ? fpool.as<uint64_t>() : nullptr;
         a.walks = walks.as<uint32_t>();
         a.rtab = rtab.as<uint64_t>();
         a.bitmap = bitmap.as<uint32_t>();
@@ -303,7 +361,7 @@ void free_handle(wharf_handle* h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->s) (void)hipStreamSynchronize(h->s);
-    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
+    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->fdir, &h->fpool, &h->fplan, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
                       &h->aff, &h->rtab, &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags,
                       &h->chg, &h->cf, &h->runstart, &h->runs, &h->rtabs, &h->count, &h->pairs, &h->sel, &h->defer, &h->esave})
         b->release();
@@ -498,6 +556,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
                                         h->ehash_mask, s);
                 if (insert) h->ehash_used += total_chg;
             }
+            h->update_filters(h->runs.as<RunInfo>(), k);
         }
         HIPCHK(hipGetLastError());   // a failed launch of the CSR pipeline surfaces here
         HIPCHK(hipEventRecord(h->ev[1], s));
@@ -1030,10 +1089,10 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     const uint64_t anchor_part = h->anchors ? h->erec.cap / 2 : 0;   // bytes 16-31 of the 32-B records
     r.records_bytes -= anchor_part;
     r.samplers_bytes = anchor_part + h->row_epoch.cap;
-    r.edge_hash_bytes = h->ehash.cap;
+    r.edge_hash_bytes = h->ehash.cap + h->fdir.cap + h->fpool.cap;
     r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->anchor2.cap + h->erec2.cap;
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
-                      h->runs.cap + h->rtabs.cap + h->count.cap + h->pairs.cap + h->sel.cap + h->defer.cap + h->esave.cap + h->rtab.cap +
+                      h->runs.cap + h->fplan.cap + h->rtabs.cap + h->count.cap + h->pairs.cap + h->sel.cap + h->defer.cap + h->esave.cap + h->rtab.cap +
                       h->bitmap.cap + h->counters.cap + h->errflag.cap;
     r.total_bytes = r.csr_bytes + r.records_bytes + r.walks_bytes + r.samplers_bytes + r.edge_hash_bytes +
                     r.update_buffers_bytes + r.scratch_bytes;

@@ -44,6 +44,17 @@ constexpr uint64_t kAnchorNone64 = ~0ull;
 constexpr uint64_t kAnchorStride = 4;         // u64 words between anchor entries (32-B node2vec edge records)
 constexpr uint64_t kEmptyKey = ~0ull;         // empty slot of the edge hash set
 constexpr uint64_t kTombKey = ~0ull - 1;      // deleted edge (probing continues past it)
+constexpr uint64_t kFiltOffBits = 48;         // neighbour-filter directory: word offset | log2(words) << 48
+constexpr uint64_t kFiltOffMask = (1ull << kFiltOffBits) - 1;
+
+// words of a row's neighbour filter: the power of two >= deg / 8 (8-16 bits per neighbour)
+__host__ __device__ __forceinline__ uint32_t filt_log2_words(uint64_t deg)
+{
+    const uint64_t w = (deg + 7) / 8;
+    uint32_t lg = 0;
+    while ((1ull << lg) < w) lg++;
+    return lg;
+}
 
 __host__ __device__ __forceinline__ ERec make_rec(uint32_t v, uint32_t deg, uint64_t off, uint32_t epoch)
 {

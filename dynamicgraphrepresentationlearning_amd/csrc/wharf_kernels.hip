@@ -65,6 +65,42 @@ __device__ __forceinline__ bool has_edge(const WalkArgs& a, const Row& rprev, ui
     }
 }
 
+// Per-row neighbour filter (a Bloom filter of each row's targets) in front of
+// has_edge in anchor inits.  Row u owns 2^k 64-bit words of `fpool` at
+// fdir[u] = word offset | k << 48, 8-16 bits per neighbour; target c sets 3
+// bits of one word.  No false negatives, so has_edge's answer is unchanged; a
+// negative (most proposals: triangles are rare) saves the random 32-B bucket
+// read of the edge hash, and the ~18 probes of one init all land in prev's
+// deg/64-byte filter (2.8 distinct lines on average, visit-weighted, for the
+// RMAT graphs of configs[1]) instead of ~18 random buckets.
+__device__ __forceinline__ uint64_t filt_hash(uint32_t c)
+{
+    uint64_t h = (uint64_t)c * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 31;
+    h *= 0xD6E8FEB86659FD93ull;
+    h ^= h >> 32;
+    return h;
+}
+__device__ __forceinline__ uint64_t filt_bits(uint64_t h)
+{
+    return (1ull << (h & 63)) | (1ull << ((h >> 6) & 63)) | (1ull << ((h >> 12) & 63));
+}
+__device__ __forceinline__ uint64_t filt_word(uint64_t fd, uint64_t h)
+{
+    return (fd & kFiltOffMask) + ((h >> 32) & ((1ull << (fd >> kFiltOffBits)) - 1));
+}
+
+// has_edge(prev, c) with prev's filter descriptor fd (fdir[prev.v]) loaded once per init
+__device__ __forceinline__ bool has_edge_filtered(const WalkArgs& a, const Row& rprev, uint64_t fd, uint32_t c)
+{
+    if (a.fpool) {
+        const uint64_t h = filt_hash(c);
+        const uint64_t b = filt_bits(h);
+        if ((a.fpool[filt_word(fd, h)] & b) != b) return false;
+    }
+    return has_edge(a, rprev, c);
+}
+
 // node2vec.h:74-88 (DeepWalk: deepwalk.h:67-70 returns 1); rprev = row of prev.
 // Weight class: 0 -> 1/p (return), 1 -> 1 (triangle), 2 -> 1/q (outward).
 template <int MODEL>
@@ -108,6 +144,8 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
         const float wtop = fmaxf(1.0f, a.inv_q);   // best weight a non-return proposal can have
         float best = 0.0f;
         uint32_t last = 0, lcls = 2;
+        const bool use_f = a.fpool && a.inv_q != 1.0f;   // prev's neighbour filter
+        const uint64_t fd = use_f ? a.fdir[rp.v] : 0;
         for (uint32_t g = 0; g < kWeightProposals; g += kProposalGroup) {
             uint32_t slot[kProposalGroup], cv[kProposalGroup];
 #pragma unroll
@@ -118,6 +156,21 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
             }
 #pragma unroll
             for (uint32_t k = 0; k < kProposalGroup; k++) cv[k] = a.adj[rc.off + slot[k]];
+            // the group's filter words in one round of independent loads (skipped once
+            // only a return proposal can still win)
+            uint32_t maybe = (1u << kProposalGroup) - 1;
+            if (use_f && !(g > 0 && best >= wtop)) {
+                uint64_t fw[kProposalGroup], fb[kProposalGroup];
+#pragma unroll
+                for (uint32_t k = 0; k < kProposalGroup; k++) {
+                    const uint64_t h = filt_hash(cv[k]);
+                    fb[k] = filt_bits(h);
+                    fw[k] = a.fpool[filt_word(fd, h)];
+                }
+                maybe = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < kProposalGroup; k++) maybe |= (uint32_t)((fw[k] & fb[k]) == fb[k]) << k;
+            }
 #pragma unroll
             for (uint32_t k = 0; k < kProposalGroup; k++) {
                 const uint32_t j = g + k;
@@ -127,8 +180,10 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
                     c = 0;
                 } else {
                     if (j > 0 && best >= wtop) continue;   // cannot be strictly greater
-                    // q == 1: triangle and outward weigh the same, the class cannot matter
-                    c = a.inv_q == 1.0f ? 1u : (has_edge(a, rp, cv[k]) ? 1u : 2u);
+                    // q == 1: triangle and outward weigh the same, the class cannot matter;
+                    // a filter negative is exact (no false negatives)
+                    c = a.inv_q == 1.0f || ((maybe >> k) & 1u) == 0 ? (a.inv_q == 1.0f ? 1u : 2u)
+                                                                    : (has_edge(a, rp, cv[k]) ? 1u : 2u);
                 }
                 const float w = class_weight(a, c);
                 if (j == 0 || w > best) { best = w; last = slot[k]; lcls = c; }
@@ -141,6 +196,7 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
     uint32_t last = (uint32_t)pick32(r.x0, rc.deg);
     uint32_t lcls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + last]);
     if (a.init == kInitBurnin) {
+        const uint64_t fd = a.fpool ? a.fdir[rp.v] : 0;
         // 100 MH moves (metropolis_hastings_sampler.h:96-104); the current
         // anchor's class is carried instead of re-probed, and a candidate's
         // has_edge is skipped when it is rejected whatever its class
@@ -157,7 +213,7 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
             }
             const bool m_tri = move(1.0f), m_out = move(a.inv_q);
             if (!m_tri && !m_out) continue;   // rejected whatever the class
-            const uint32_t c = has_edge(a, rp, cv) ? 1u : 2u;
+            const uint32_t c = has_edge_filtered(a, rp, fd, cv) ? 1u : 2u;
             if (c == 1 ? m_tri : m_out) { last = cand; lcls = c; }
         }
     }
@@ -695,6 +751,105 @@ void launch_edge_hash_build(const uint64_t* off, uint64_t n, const uint32_t* adj
 {
     if (n) hipLaunchKernelGGL(k_edge_hash_build, (unsigned)((n + 63) / 64), 256, 0, s, off, n, adj,
                               (unsigned long long*)table, mask);
+}
+
+// ---------------------------------------------------------------------------
+// Neighbour filters (see has_edge_filtered): sizes, directory, fill; per batch
+// only the source rows are rebuilt (a row that outgrows its words gets new
+// ones at the end of the pool)
+// ---------------------------------------------------------------------------
+__global__ void k_filter_sizes(const uint64_t* __restrict__ off, uint64_t n, uint64_t* __restrict__ words)
+{
+    for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= n; u += (uint64_t)gridDim.x * blockDim.x)
+        words[u] = u < n ? 1ull << filt_log2_words(off[u + 1] - off[u]) : 0;
+}
+
+__global__ void k_filter_pack(const uint64_t* __restrict__ off, uint64_t n, uint64_t* __restrict__ fdir)
+{
+    for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n; u += (uint64_t)gridDim.x * blockDim.x)
+        fdir[u] |= (uint64_t)filt_log2_words(off[u + 1] - off[u]) << kFiltOffBits;
+}
+
+__device__ __forceinline__ void filter_set(unsigned long long* pool, uint64_t fd, uint32_t c)
+{
+    const uint64_t h = filt_hash(c);
+    atomicOr(pool + filt_word(fd, h), (unsigned long long)filt_bits(h));
+}
+
+// one wave per row, lanes sweep the row's targets (as k_edge_hash_build)
+__global__ void k_filter_fill(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ adj,
+                              const uint64_t* __restrict__ fdir, unsigned long long* __restrict__ pool)
+{
+    const uint64_t v0 = (uint64_t)blockIdx.x * 64;
+    for (uint64_t u = v0 + threadIdx.x / 64; u < min(v0 + 64, n); u += blockDim.x / 64) {
+        const uint64_t b0 = off[u], e0 = off[u + 1], fd = fdir[u];
+        for (uint64_t j = b0 + (threadIdx.x & 63); j < e0; j += 64) filter_set(pool, fd, adj[j]);
+    }
+}
+
+// per batch source: words its new row needs when it outgrew its old ones, else 0
+__global__ void k_filter_plan(const RunInfo* __restrict__ runs, uint64_t k, const uint64_t* __restrict__ noff,
+                              const uint64_t* __restrict__ fdir, uint64_t* __restrict__ need)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= k; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (i == k) { need[i] = 0; continue; }
+        const uint32_t u = runs[i].src;
+        const uint32_t lg = filt_log2_words(noff[u + 1] - noff[u]);
+        need[i] = lg > (uint32_t)(fdir[u] >> kFiltOffBits) ? 1ull << lg : 0;
+    }
+}
+
+// one block per batch source: (re)place, clear and refill its filter from the new row
+__global__ void k_filter_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ noff,
+                              const uint32_t* __restrict__ adj, const uint64_t* __restrict__ need,
+                              const uint64_t* __restrict__ gofs, uint64_t base, uint64_t* __restrict__ fdir,
+                              unsigned long long* __restrict__ pool)
+{
+    const uint64_t i = blockIdx.x;
+    const uint32_t u = runs[i].src;
+    uint64_t fd = fdir[u];
+    if (need[i]) {
+        const uint32_t lg = filt_log2_words(noff[u + 1] - noff[u]);
+        fd = (base + gofs[i]) | ((uint64_t)lg << kFiltOffBits);
+        __syncthreads();   // every thread has read the old descriptor
+        if (threadIdx.x == 0) fdir[u] = fd;
+    }
+    const uint64_t w0 = fd & kFiltOffMask, nw = 1ull << (fd >> kFiltOffBits);
+    for (uint64_t j = threadIdx.x; j < nw; j += blockDim.x) pool[w0 + j] = 0;
+    __threadfence();
+    __syncthreads();
+    for (uint64_t j = noff[u] + threadIdx.x; j < noff[u + 1]; j += blockDim.x) filter_set(pool, fd, adj[j]);
+}
+
+void launch_filter_sizes(const uint64_t* off, uint64_t n, uint64_t* words, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_filter_sizes, grid_for(n + 1, 256), 256, 0, s, off, n, words);
+}
+
+void launch_filter_pack(const uint64_t* off, uint64_t n, uint64_t* fdir, hipStream_t s)
+{
+    if (n) hipLaunchKernelGGL(k_filter_pack, grid_for(n, 256), 256, 0, s, off, n, fdir);
+}
+
+void launch_filter_fill(const uint64_t* off, uint64_t n, const uint32_t* adj, const uint64_t* fdir, uint64_t* pool,
+                        hipStream_t s)
+{
+    if (n) hipLaunchKernelGGL(k_filter_fill, (unsigned)((n + 63) / 64), 256, 0, s, off, n, adj, fdir,
+                              (unsigned long long*)pool);
+}
+
+void launch_filter_plan(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint64_t* fdir, uint64_t* need,
+                        hipStream_t s)
+{
+    hipLaunchKernelGGL(k_filter_plan, grid_for(k + 1, 256), 256, 0, s, runs, k, noff, fdir, need);
+}
+
+void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* adj,
+                        const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir, uint64_t* pool,
+                        hipStream_t s)
+{
+    if (k) hipLaunchKernelGGL(k_filter_rows, (unsigned)k, 256, 0, s, runs, noff, adj, need, gofs, base, fdir,
+                              (unsigned long long*)pool);
 }
 
 __global__ void k_csr_to_keys(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ tgt,

@@ -182,7 +182,7 @@ typedef struct wharf_memory {
     uint64_t records_bytes;         /* vertex + edge row records */
     uint64_t walks_bytes;           /* walk matrix + per-walk rewalk positions (the walk trees) */
     uint64_t samplers_bytes;        /* MH anchors + per-row sampler epochs (the samplers) */
-    uint64_t edge_hash_bytes;       /* node2vec has_edge set */
+    uint64_t edge_hash_bytes;       /* node2vec has_edge set + per-row neighbour filters */
     uint64_t update_buffers_bytes;  /* second CSR / record buffers of the batch merge */
     uint64_t scratch_bytes;         /* sort / select temporaries, batch and draw tables */
     uint64_t total_bytes;

@@ -306,9 +306,9 @@ def test_affected_ids_on_device_match_host_list(W):
     gd.destroy()
 
 
-# (WHARF_LOCKSTEP_MIN, WHARF_MOVE_NO_LDS, WHARF_FORCE_RECORD_REBUILD)
-PATHS = {"sweep/patch-lds": ("0", "0", "0"), "deferred/inplace-l2": ("65", "1", "1"),
-         "mixed/inplace-lds": ("40", "0", "1"), "mixed/gather": ("16", "1", "2")}
+# (WHARF_LOCKSTEP_MIN, WHARF_MOVE_NO_LDS, WHARF_FORCE_RECORD_REBUILD, neighbour filter)
+PATHS = {"sweep/patch-lds": ("0", "0", "0", "on"), "deferred/inplace-l2": ("65", "1", "1", "noslack"),
+         "mixed/inplace-lds": ("40", "0", "1", "off"), "mixed/gather": ("16", "1", "2", "on")}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -321,8 +321,13 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     defers) and a mix.  CSR update: the record patch with the source table in
     LDS or the bucketed L2 table (WHARF_MOVE_NO_LDS), into a second record
     buffer, in place (chunked), or records rebuilt by a gather with node2vec
-    anchors kept aside (WHARF_FORCE_RECORD_REBUILD=1 / 2)."""
-    lockstep_min, no_lds, force = PATHS[path]
+    anchors kept aside (WHARF_FORCE_RECORD_REBUILD=1 / 2).  node2vec anchor
+    inits with the per-row neighbour filters (re-filled per source row, or with
+    no pool headroom re-built whole whenever a row outgrows its words) and
+    without them."""
+    lockstep_min, no_lds, force, filt = PATHS[path]
+    monkeypatch.setenv("WHARF_NO_NEIGHBOUR_FILTER", "1" if filt == "off" else "0")
+    monkeypatch.setenv("WHARF_FILTER_NO_SLACK", "1" if filt == "noslack" else "0")
     monkeypatch.setenv("WHARF_LOCKSTEP_MIN", lockstep_min)
     monkeypatch.setenv("WHARF_MOVE_NO_LDS", no_lds)
     monkeypatch.setenv("WHARF_FORCE_RECORD_REBUILD", force)

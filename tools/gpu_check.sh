@@ -39,6 +39,9 @@ for s in "$@"; do
     c4)     step c4_stream 1100 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 50 ;;
     c5n2v)  step c5_node2vec 1100 python tools/bigscale.py --model node2vec --wpv 1 --batches 10 --mixed ;;
     det)    step bench_det 900 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
+    n2vnf)  step bench_n2v_nofilter 900 env WHARF_NO_NEIGHBOUR_FILTER=1 python bench.py --model node2vec --steps 2 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
+    c5n2vnf) step c5_node2vec_nofilter 1100 env WHARF_NO_NEIGHBOUR_FILTER=1 python tools/bigscale.py --model node2vec --wpv 1 --batches 4 --mixed --no-oracle ;;
+    c5n2vq) step c5_node2vec_q 1100 python tools/bigscale.py --model node2vec --wpv 1 --batches 4 --mixed --no-oracle ;;
     n2v)    step bench_n2v 900 python bench.py --model node2vec --steps 2 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     dist2)  step bench_dist2 900 env WHARF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --scale 20 --samples 29296270 --stream-samples 10000000 --steps 3 --warmup 1 --rewalk-batches 5 ;;
     dist2full) step bench_dist2_full 900 env WHARF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --rewalk-batches 5 ;;
