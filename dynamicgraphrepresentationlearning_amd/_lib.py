@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwharf_gpu.so")
+# WHARF_LIB_PATH: an alternative build of the same library (A/B experiments in tools/)
+LIB_PATH = os.environ.get("WHARF_LIB_PATH") or os.path.join(_HERE, "libwharf_gpu.so")
 
 WHARF_OK = 0
 WHARF_DEEPWALK, WHARF_NODE2VEC = 0, 1

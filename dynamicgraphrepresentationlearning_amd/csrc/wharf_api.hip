@@ -205,13 +205,13 @@ struct wharf_handle {
         words.release();
         // WHARF_FILTER_NO_SLACK (tests): no headroom, so every row that outgrows its words re-builds all
         const char* ns = getenv("WHARF_FILTER_NO_SLACK");
-        const uint64_t want = std::max<uint64_t>(ns && atoi(ns) ? total : total + total / 4, 1) * 8;
+        const uint64_t want = std::max<uint64_t>(ns && atoi(ns) ? total : total + total / 4, 1) * 4;
         if (fpool.cap > want + want / 2) fpool.release();   // do not keep a much larger pool
         fpool.ensure(want);
         fpool_used = total;
-        HIPCHK(hipMemsetAsync(fpool.p, 0, total * 8, s));
+        HIPCHK(hipMemsetAsync(fpool.p, 0, total * 4, s));
         launch_filter_pack(off.as<uint64_t>(), n, fdir.as<uint64_t>(), s);
-        launch_filter_fill(off.as<uint64_t>(), n, adj.as<uint32_t>(), fdir.as<uint64_t>(), fpool.as<uint64_t>(), s);
+        launch_filter_fill(off.as<uint64_t>(), n, adj.as<uint32_t>(), fdir.as<uint64_t>(), fpool.as<uint32_t>(), s);
     }
 
     // after a batch: rebuild the filters of the k batch sources from their new rows
@@ -228,12 +228,12 @@ struct wharf_handle {
         uint64_t grow = 0;
         HIPCHK(hipMemcpyAsync(&grow, gofs + k, 8, hipMemcpyDeviceToHost, s));
         sync();
-        if (fpool_used + grow > fpool.cap / 8) {
+        if (fpool_used + grow > fpool.cap / 4) {
             build_filters();   // out of headroom: re-size and re-fill every row (drops the gaps)
             return;
         }
         launch_filter_rows(runs_d, k, off.as<uint64_t>(), adj.as<uint32_t>(), need, gofs, fpool_used,
-                           fdir.as<uint64_t>(), fpool.as<uint64_t>(), s);
+                           fdir.as<uint64_t>(), fpool.as<uint32_t>(), s);
         fpool_used += grow;
     }
 
@@ -248,7 +248,7 @@ struct wharf_handle {
         a.ehash = anchors ? ehash.as<uint64_t>() : nullptr;
         a.ehash_mask = ehash_mask;
         a.fdir = anchors && fpool.p ? fdir.as<uint64_t>() : nullptr;
-        a.fpool = anchors && fpool.p ? fpool.as<uint64_t>() : nullptr;
+        a.fpool = anchors && fpool.p ? fpool.as<uint32_t>() : nullptr;
         a.walks = walks.as<uint32_t>();
         a.rtab = rtab.as<uint64_t>();
         a.bitmap = bitmap.as<uint32_t>();

@@ -47,10 +47,10 @@ constexpr uint64_t kTombKey = ~0ull - 1;      // deleted edge (probing continues
 constexpr uint64_t kFiltOffBits = 48;         // neighbour-filter directory: word offset | log2(words) << 48
 constexpr uint64_t kFiltOffMask = (1ull << kFiltOffBits) - 1;
 
-// words of a row's neighbour filter: the power of two >= deg / 8 (8-16 bits per neighbour)
+// 32-bit words of a row's neighbour filter: the power of two >= deg / 4 (8-16 bits per neighbour)
 __host__ __device__ __forceinline__ uint32_t filt_log2_words(uint64_t deg)
 {
-    const uint64_t w = (deg + 7) / 8;
+    const uint64_t w = (deg + 3) / 4;
     uint32_t lg = 0;
     while ((1ull << lg) < w) lg++;
     return lg;

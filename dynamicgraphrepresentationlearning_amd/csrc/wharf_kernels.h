@@ -23,7 +23,7 @@ struct WalkArgs {
     const uint64_t* ehash;       // node2vec: edge hash set (u << 32 | v), or null -> binary search
     uint64_t ehash_mask;         // capacity - 1 (power of two)
     const uint64_t* fdir;        // node2vec MH: per-row neighbour filter {word offset | log2 words << 48}, or null
-    const uint64_t* fpool;       //   and its words (filter_maybe in front of has_edge in anchor inits)
+    const uint32_t* fpool;       //   and its 32-bit words (in front of has_edge in anchor inits)
     uint32_t* walks;             // [L][W]
     const uint64_t* rtab;        // deterministic draws [wpv][L]
     const uint32_t* bitmap;      // batch sources (re-walk)
@@ -125,12 +125,12 @@ void launch_edge_hash_build(const uint64_t* off, uint64_t n, const uint32_t* adj
                             hipStream_t s);
 void launch_filter_sizes(const uint64_t* off, uint64_t n, uint64_t* words, hipStream_t s);
 void launch_filter_pack(const uint64_t* off, uint64_t n, uint64_t* fdir, hipStream_t s);
-void launch_filter_fill(const uint64_t* off, uint64_t n, const uint32_t* adj, const uint64_t* fdir, uint64_t* pool,
+void launch_filter_fill(const uint64_t* off, uint64_t n, const uint32_t* adj, const uint64_t* fdir, uint32_t* pool,
                         hipStream_t s);
 void launch_filter_plan(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint64_t* fdir, uint64_t* need,
                         hipStream_t s);
 void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* adj,
-                        const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir, uint64_t* pool,
+                        const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir, uint32_t* pool,
                         hipStream_t s);
 void launch_szudzik64(int op, uint64_t cnt, uint64_t* x, uint64_t* y, uint64_t* z, hipStream_t s);
 

@@ -66,12 +66,12 @@ __device__ __forceinline__ bool has_edge(const WalkArgs& a, const Row& rprev, ui
 }
 
 // Per-row neighbour filter (a Bloom filter of each row's targets) in front of
-// has_edge in anchor inits.  Row u owns 2^k 64-bit words of `fpool` at
+// has_edge in anchor inits.  Row u owns 2^k 32-bit words of `fpool` at
 // fdir[u] = word offset | k << 48, 8-16 bits per neighbour; target c sets 3
 // bits of one word.  No false negatives, so has_edge's answer is unchanged; a
 // negative (most proposals: triangles are rare) saves the random 32-B bucket
 // read of the edge hash, and the ~18 probes of one init all land in prev's
-// deg/64-byte filter (2.8 distinct lines on average, visit-weighted, for the
+// deg-byte filter (2.8 distinct lines on average, visit-weighted, for the
 // RMAT graphs of configs[1]) instead of ~18 random buckets.
 __device__ __forceinline__ uint64_t filt_hash(uint32_t c)
 {
@@ -81,9 +81,9 @@ __device__ __forceinline__ uint64_t filt_hash(uint32_t c)
     h ^= h >> 32;
     return h;
 }
-__device__ __forceinline__ uint64_t filt_bits(uint64_t h)
+__device__ __forceinline__ uint32_t filt_bits(uint64_t h)
 {
-    return (1ull << (h & 63)) | (1ull << ((h >> 6) & 63)) | (1ull << ((h >> 12) & 63));
+    return (1u << (h & 31)) | (1u << ((h >> 5) & 31)) | (1u << ((h >> 10) & 31));
 }
 __device__ __forceinline__ uint64_t filt_word(uint64_t fd, uint64_t h)
 {
@@ -95,7 +95,7 @@ __device__ __forceinline__ bool has_edge_filtered(const WalkArgs& a, const Row& 
 {
     if (a.fpool) {
         const uint64_t h = filt_hash(c);
-        const uint64_t b = filt_bits(h);
+        const uint32_t b = filt_bits(h);
         if ((a.fpool[filt_word(fd, h)] & b) != b) return false;
     }
     return has_edge(a, rprev, c);
@@ -135,7 +135,10 @@ __device__ __forceinline__ float weight(const WalkArgs& a, const Row& rprev, uin
 // step, with ~18 has_edge calls each: triangle and return proposals are rare
 // on RMAT graphs.  Scanning all proposals for a return first, which needs no
 // lookup, cost more than it saved: 151 -> 185 ms.)
-constexpr uint32_t kWeightProposals = 21, kProposalGroup = 4;
+#ifndef WHARF_PROPOSAL_GROUP
+#define WHARF_PROPOSAL_GROUP 4
+#endif
+constexpr uint32_t kWeightProposals = 21, kProposalGroup = WHARF_PROPOSAL_GROUP;
 
 __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp, uint32_t& cls)
 {
@@ -160,7 +163,7 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
             // only a return proposal can still win)
             uint32_t maybe = (1u << kProposalGroup) - 1;
             if (use_f && !(g > 0 && best >= wtop)) {
-                uint64_t fw[kProposalGroup], fb[kProposalGroup];
+                uint32_t fw[kProposalGroup], fb[kProposalGroup];
 #pragma unroll
                 for (uint32_t k = 0; k < kProposalGroup; k++) {
                     const uint64_t h = filt_hash(cv[k]);
@@ -770,15 +773,15 @@ __global__ void k_filter_pack(const uint64_t* __restrict__ off, uint64_t n, uint
         fdir[u] |= (uint64_t)filt_log2_words(off[u + 1] - off[u]) << kFiltOffBits;
 }
 
-__device__ __forceinline__ void filter_set(unsigned long long* pool, uint64_t fd, uint32_t c)
+__device__ __forceinline__ void filter_set(uint32_t* pool, uint64_t fd, uint32_t c)
 {
     const uint64_t h = filt_hash(c);
-    atomicOr(pool + filt_word(fd, h), (unsigned long long)filt_bits(h));
+    atomicOr(pool + filt_word(fd, h), filt_bits(h));
 }
 
 // one wave per row, lanes sweep the row's targets (as k_edge_hash_build)
 __global__ void k_filter_fill(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ adj,
-                              const uint64_t* __restrict__ fdir, unsigned long long* __restrict__ pool)
+                              const uint64_t* __restrict__ fdir, uint32_t* __restrict__ pool)
 {
     const uint64_t v0 = (uint64_t)blockIdx.x * 64;
     for (uint64_t u = v0 + threadIdx.x / 64; u < min(v0 + 64, n); u += blockDim.x / 64) {
@@ -803,7 +806,7 @@ __global__ void k_filter_plan(const RunInfo* __restrict__ runs, uint64_t k, cons
 __global__ void k_filter_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ noff,
                               const uint32_t* __restrict__ adj, const uint64_t* __restrict__ need,
                               const uint64_t* __restrict__ gofs, uint64_t base, uint64_t* __restrict__ fdir,
-                              unsigned long long* __restrict__ pool)
+                              uint32_t* __restrict__ pool)
 {
     const uint64_t i = blockIdx.x;
     const uint32_t u = runs[i].src;
@@ -831,11 +834,10 @@ void launch_filter_pack(const uint64_t* off, uint64_t n, uint64_t* fdir, hipStre
     if (n) hipLaunchKernelGGL(k_filter_pack, grid_for(n, 256), 256, 0, s, off, n, fdir);
 }
 
-void launch_filter_fill(const uint64_t* off, uint64_t n, const uint32_t* adj, const uint64_t* fdir, uint64_t* pool,
+void launch_filter_fill(const uint64_t* off, uint64_t n, const uint32_t* adj, const uint64_t* fdir, uint32_t* pool,
                         hipStream_t s)
 {
-    if (n) hipLaunchKernelGGL(k_filter_fill, (unsigned)((n + 63) / 64), 256, 0, s, off, n, adj, fdir,
-                              (unsigned long long*)pool);
+    if (n) hipLaunchKernelGGL(k_filter_fill, (unsigned)((n + 63) / 64), 256, 0, s, off, n, adj, fdir, pool);
 }
 
 void launch_filter_plan(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint64_t* fdir, uint64_t* need,
@@ -845,11 +847,10 @@ void launch_filter_plan(const RunInfo* runs, uint64_t k, const uint64_t* noff, c
 }
 
 void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* adj,
-                        const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir, uint64_t* pool,
+                        const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir, uint32_t* pool,
                         hipStream_t s)
 {
-    if (k) hipLaunchKernelGGL(k_filter_rows, (unsigned)k, 256, 0, s, runs, noff, adj, need, gofs, base, fdir,
-                              (unsigned long long*)pool);
+    if (k) hipLaunchKernelGGL(k_filter_rows, (unsigned)k, 256, 0, s, runs, noff, adj, need, gofs, base, fdir, pool);
 }
 
 __global__ void k_csr_to_keys(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ tgt,
