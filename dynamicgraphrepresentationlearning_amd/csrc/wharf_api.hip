@@ -87,6 +87,7 @@ struct wharf_handle {
     DevBuf off, adj, vrec, erec, row_epoch, off2, adj2, anchor2, ehash, erec2;
     uint64_t ehash_mask = 0, ehash_used = 0;   // capacity - 1; occupied slots incl. tombstones
     DevBuf fdir, fpool, fplan;                 // node2vec MH: per-row neighbour filters (k_filter_*)
+    DevBuf memo, srcidx;                       // deterministic re-walk: suffix table, source index
     uint64_t fpool_used = 0;                   // words handed out (rows that outgrew theirs leave gaps)
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
     DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, rtabs, count, pairs, sel, defer, esave;
@@ -255,7 +256,7 @@ struct wharf_handle {
         a.bloom = bitmap.as<uint32_t>() + bitmap_words();
         a.aff = aff.as<uint8_t>();
         a.counters = counters.as<unsigned long long>();
-        a.n = n; a.n_loc = n_loc; a.lo = lo; a.W = W;
+        a.n = n; a.n_loc = n_loc; a.lo = lo; a.W = W; a.wpv = wpv;
         a.L = L; a.epoch = epoch;
         a.key0 = (uint32_t)cfg.seed; a.key1 = (uint32_t)(cfg.seed >> 32);
         a.inv_p = 1.0f / cfg.paramP;   // node2vec.h:81 `1 / this->paramP` in float
@@ -361,7 +362,7 @@ void free_handle(wharf_handle* h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->s) (void)hipStreamSynchronize(h->s);
-    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->fdir, &h->fpool, &h->fplan, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
+    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->fdir, &h->fpool, &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
                       &h->aff, &h->rtab, &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags,
                       &h->chg, &h->cf, &h->runstart, &h->runs, &h->rtabs, &h->count, &h->pairs, &h->sel, &h->defer, &h->esave})
         b->release();
@@ -568,6 +569,22 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             WalkArgs a = h->walk_args();
             a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
             a.lockstep_min = lockstep_min();
+            // deterministic mode: suffixes walked once per (round, batch source) and copied
+            // (k_det_suffix + k_rewalk_memo) while the table stays small; WHARF_NO_MEMO=1 (tests)
+            // re-walks every suffix (k_rewalk_sweep)
+            const uint64_t stride4 = (h->L + 3) & ~3ull;
+            const char* no_memo = getenv("WHARF_NO_MEMO");
+            if (a.det && !a.scan_only && k && !(no_memo && atoi(no_memo)) &&
+                (uint64_t)h->wpv * k * stride4 * 4 <= (256ull << 20)) {
+                h->srcidx.ensure(std::max<uint64_t>(h->n, 1) * 4);
+                h->memo.ensure((uint64_t)h->wpv * k * stride4 * 4);
+                launch_src_index(h->runs.as<RunInfo>(), k, h->srcidx.as<uint32_t>(), s);
+                a.memo = h->memo.as<uint32_t>();
+                a.src_idx = h->srcidx.as<uint32_t>();
+                a.runs = h->runs.as<RunInfo>();
+                a.memo_k = k;
+                a.memo_stride = (uint32_t)stride4;
+            }
             if (!a.scan_only && a.lockstep_min > 0 && a.model == kNode2Vec && !a.det) {   // k_rewalk_list
                 h->defer.ensure(h->W * 8);
                 a.defer = h->defer.as<uint64_t>();
@@ -1092,7 +1109,7 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     r.edge_hash_bytes = h->ehash.cap + h->fdir.cap + h->fpool.cap;
     r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->anchor2.cap + h->erec2.cap;
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
-                      h->runs.cap + h->fplan.cap + h->rtabs.cap + h->count.cap + h->pairs.cap + h->sel.cap + h->defer.cap + h->esave.cap + h->rtab.cap +
+                      h->runs.cap + h->fplan.cap + h->memo.cap + h->srcidx.cap + h->rtabs.cap + h->count.cap + h->pairs.cap + h->sel.cap + h->defer.cap + h->esave.cap + h->rtab.cap +
                       h->bitmap.cap + h->counters.cap + h->errflag.cap;
     r.total_bytes = r.csr_bytes + r.records_bytes + r.walks_bytes + r.samplers_bytes + r.edge_hash_bytes +
                     r.update_buffers_bytes + r.scratch_bytes;

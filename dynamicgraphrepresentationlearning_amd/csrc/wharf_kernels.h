@@ -14,6 +14,11 @@ namespace wharf {
 enum { kDeepWalk = 0, kNode2Vec = 1 };
 enum { kInitRandom = 0, kInitBurnin = 1, kInitWeight = 2 };
 
+struct RunInfo {
+    uint64_t off, end;   // old row [off, end)
+    uint32_t src, rs, re, pad;
+};
+
 struct WalkArgs {
     const ERec* vrec;            // [n]: the row of each vertex
     const ERec* erec;            // [m]: per CSR slot, the target's row
@@ -38,12 +43,15 @@ struct WalkArgs {
     int scan_only;               // re-walk: only find rewalk points (apply_walk_updates=false)
     uint64_t* defer;             // re-walk: walks of sparse waves, {li | p << 56}, count in counters[2]
     uint32_t lockstep_min;       // re-walk: a wave with fewer affected walks defers them to `defer`
+    // deterministic re-walk by suffix table (k_det_suffix + k_rewalk_memo), or memo == null
+    uint32_t* memo;              // [wpv][k][memo_stride]: walk from batch source i in round r, new graph
+    const uint32_t* src_idx;     // [n]: index of a batch source in the run table (read for sources only)
+    const RunInfo* runs;         // the batch's source runs
+    uint64_t memo_k;             // sources (runs) in the batch
+    uint32_t memo_stride;        // L rounded up to 4 (16-B aligned rows)
+    uint32_t wpv;
 };
 
-struct RunInfo {
-    uint64_t off, end;   // old row [off, end)
-    uint32_t src, rs, re, pad;
-};
 
 // bucketed lookup tables over the source-run table (k_run_tables)
 struct RunIndex {
@@ -70,6 +78,7 @@ unsigned grid_for(uint64_t work, unsigned block);
 unsigned cu_count();
 
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s);
+void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStream_t s);
 void launch_vrec(const uint64_t* off, uint64_t n, const uint32_t* row_epoch, ERec* vrec, hipStream_t s);
 void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s);
 void launch_anchor_merge(const uint64_t* src, uint64_t m, uint64_t* dst, hipStream_t s);

@@ -482,6 +482,107 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
     wave_add(a.counters + 1, accepts);
 }
 
+// Deterministic re-walk by suffix table.  In deterministic mode a re-walk
+// from (vertex s, position p) of a round-r walk draws Random(r) from draw 0
+// again (wharfmh.h:813-840), so its suffix depends only on (r, s): it is the
+// first L-1-p steps of a walk STARTING at s in round r on the new graph.  The
+// rewalk vertex is always a batch source, so k_det_suffix walks the wpv x k
+// suffixes once (k <= 10 k distinct sources per batch) and k_rewalk_memo
+// copies them: the re-walk of ~34 M walks becomes a streaming pass over the
+// walk matrix plus reads of a small, cache-resident table, instead of one
+// random graph gather per re-walked position.  Same values, same step count.
+constexpr uint32_t kXcds = 8;   // MI355X: 8 XCDs, workgroups dispatched round-robin
+
+__global__ __launch_bounds__(256) void k_det_suffix(WalkArgs a)
+{
+    const uint64_t total = (uint64_t)a.wpv * a.memo_k;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = t / a.memo_k, i = t - r * a.memo_k;
+        const uint32_t src = a.runs[i].src;
+        uint32_t* __restrict__ out = a.memo + t * a.memo_stride;
+        const uint64_t* __restrict__ rt = a.rtab + r * a.L;
+        Walker w;
+        walk_state<kDeepWalk, true>(a, src, src, 0, 0, 0, 0, w);
+        out[0] = src;
+        uint32_t unused = 0;
+        for (uint32_t j = 1; j < a.memo_stride; j++) {
+            uint32_t val = kSent;
+            if (j < a.L && w.rc.deg) val = walk_step<kDeepWalk, true>(a, w, rt, j - 1, 0, 0, 0, unused);
+            out[j] = val;
+        }
+    }
+}
+
+// The sweep of k_rewalk_sweep (lock-step positions, full-row stores), with
+// the walking lanes reading their suffix row four positions per 16-B load.
+// XCD-aware: workgroups are placed on the 8 XCDs round-robin, so XCD x
+// (blockIdx % 8) takes the x-th eighth of the walks — ~1.25 rounds — and its
+// 4 MiB L2 holds the suffix rows of those rounds (k x L x 4 B = 3.2 MB per
+// round at 10 k sources) instead of all of them.
+__global__ __launch_bounds__(256) void k_rewalk_memo(WalkArgs a)
+{
+    __shared__ uint32_t s_bloom[kBloomWords];
+    bloom_to_lds(a, s_bloom);
+    uint32_t steps = 0;
+    uint32_t* __restrict__ walks = a.walks;
+    const uint64_t W = a.W;
+    const uint32_t L = a.L;
+    const uint32_t xcd = blockIdx.x % kXcds, slot = blockIdx.x / kXcds, per = gridDim.x / kXcds;
+    const uint64_t chunk = (W + kXcds - 1) / kXcds;
+    const uint64_t c0 = xcd * chunk, c1 = min(W, c0 + chunk);
+    const uint64_t stride = (uint64_t)per * blockDim.x;
+    for (uint64_t li = c0 + (uint64_t)slot * blockDim.x + threadIdx.x; li < c1; li += stride) {
+        const uint64_t r = li / a.n_loc;
+        const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
+        uint32_t mode = kLaneScan, p = kNoRewalk;
+        uint32_t x = v;
+        uint32_t xn = L > 1 ? walks[W + li] : kSent;   // old value at pos + 1 (prefetched)
+        const uint32_t* __restrict__ row = nullptr;
+        uint4 q = make_uint4(kSent, kSent, kSent, kSent);
+        for (uint32_t pos = 0; pos < L; pos++) {
+            uint32_t val = kSent;
+            bool fresh = false;
+            if (mode == kLaneWalk) {
+                const uint32_t j = pos - p;
+                if ((j & 3) == 0 || j == 1) q = *reinterpret_cast<const uint4*>(row + (j & ~3u));
+                const uint32_t e = j & 3;
+                val = e == 0 ? q.x : (e == 1 ? q.y : (e == 2 ? q.z : q.w));
+                steps += val != kSent;
+                fresh = true;
+            } else if (mode == kLaneScan) {
+                if (pos > 0) {
+                    x = xn;
+                    if (pos + 1 < L && x != kSent) xn = walks[(uint64_t)(pos + 1) * W + li];
+                }
+                val = x;
+                if (x == kSent) {
+                    mode = kLaneDone;
+                } else if (is_source(a, s_bloom, x)) {
+                    p = pos;
+                    mode = kLaneWalk;
+                    row = a.memo + (r * a.memo_k + a.src_idx[x]) * a.memo_stride;
+                }
+            }
+            if (__any(fresh)) walks[(uint64_t)pos * W + li] = val;
+            if (!__any(mode != kLaneDone)) break;
+        }
+        a.aff[li] = (uint8_t)p;
+    }
+    wave_add(a.counters + 0, steps);
+}
+
+__global__ void k_src_index(const RunInfo* __restrict__ runs, uint64_t k, uint32_t* __restrict__ src_idx)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < k; i += (uint64_t)gridDim.x * blockDim.x)
+        src_idx[runs[i].src] = (uint32_t)i;
+}
+
+void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStream_t s)
+{
+    if (k) hipLaunchKernelGGL(k_src_index, grid_for(k, 256), 256, 0, s, runs, k, src_idx);
+}
+
 // Fused rewalk-point scan + suffix re-walk, node2vec MH.  Setting up a
 // node2vec walker is a chain of dependent loads (rows of cur and prev, the
 // binary search for the anchor-cache slot of the edge prev -> cur), which
@@ -670,6 +771,13 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
             hipLaunchKernelGGL((k_walk<M, D>), grid, block, 0, s, a);                        \
         }                                                                                    \
     } while (0)
+    if (rewalk && a.det && a.memo && !a.scan_only) {
+        hipLaunchKernelGGL(k_det_suffix, grid_for((uint64_t)a.wpv * a.memo_k, 256), 256, 0, s, a);
+        // a multiple of 8 workgroups: every XCD gets the same number
+        const dim3 mgrid((std::max<unsigned>(grid.x, kXcds) / kXcds) * kXcds);
+        hipLaunchKernelGGL(k_rewalk_memo, mgrid, block, 0, s, a);
+        return;
+    }
     if (a.det) WHARF_LAUNCH(kDeepWalk, true);
     else if (a.model == kDeepWalk) WHARF_LAUNCH(kDeepWalk, false);
     else WHARF_LAUNCH(kNode2Vec, false);

@@ -306,9 +306,9 @@ def test_affected_ids_on_device_match_host_list(W):
     gd.destroy()
 
 
-# (WHARF_LOCKSTEP_MIN, WHARF_MOVE_NO_LDS, WHARF_FORCE_RECORD_REBUILD, neighbour filter)
-PATHS = {"sweep/patch-lds": ("0", "0", "0", "on"), "deferred/inplace-l2": ("65", "1", "1", "noslack"),
-         "mixed/inplace-lds": ("40", "0", "1", "off"), "mixed/gather": ("16", "1", "2", "on")}
+# (WHARF_LOCKSTEP_MIN, WHARF_MOVE_NO_LDS, WHARF_FORCE_RECORD_REBUILD, neighbour filter, WHARF_NO_MEMO)
+PATHS = {"sweep/patch-lds": ("0", "0", "0", "on", "1"), "deferred/inplace-l2": ("65", "1", "1", "noslack", "0"),
+         "mixed/inplace-lds": ("40", "0", "1", "off", "0"), "mixed/gather": ("16", "1", "2", "on", "1")}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -324,8 +324,10 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     anchors kept aside (WHARF_FORCE_RECORD_REBUILD=1 / 2).  node2vec anchor
     inits with the per-row neighbour filters (re-filled per source row, or with
     no pool headroom re-built whole whenever a row outgrows its words) and
-    without them."""
-    lockstep_min, no_lds, force, filt = PATHS[path]
+    without them.  Deterministic re-walks by suffix table (k_rewalk_memo) and
+    by walking every suffix (WHARF_NO_MEMO=1, k_rewalk_sweep)."""
+    lockstep_min, no_lds, force, filt, no_memo = PATHS[path]
+    monkeypatch.setenv("WHARF_NO_MEMO", no_memo)
     monkeypatch.setenv("WHARF_NO_NEIGHBOUR_FILTER", "1" if filt == "off" else "0")
     monkeypatch.setenv("WHARF_FILTER_NO_SLACK", "1" if filt == "noslack" else "0")
     monkeypatch.setenv("WHARF_LOCKSTEP_MIN", lockstep_min)

@@ -38,6 +38,7 @@ for s in "$@"; do
     index)  step index_probe 800 python tools/index_probe.py ;;
     c4)     step c4_stream 1100 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 50 ;;
     c5n2v)  step c5_node2vec 1100 python tools/bigscale.py --model node2vec --wpv 1 --batches 10 --mixed ;;
+    detnm)  step bench_det_nomemo 900 env WHARF_NO_MEMO=1 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     det)    step bench_det 900 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     n2vnf)  step bench_n2v_nofilter 900 env WHARF_NO_NEIGHBOUR_FILTER=1 python bench.py --model node2vec --steps 2 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     c5n2vnf) step c5_node2vec_nofilter 1100 env WHARF_NO_NEIGHBOUR_FILTER=1 python tools/bigscale.py --model node2vec --wpv 1 --batches 4 --mixed --no-oracle ;;
