@@ -50,6 +50,12 @@ for s in "$@"; do
     pmc)    step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 0 --rewalk-batches 0 --cpu-baseline off
             step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 0 --rewalk-batches 0 --cpu-baseline off
             step pmc_req 900 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/pmc_req -o run -- python3 bench.py --steps 2 --warmup 0 --rewalk-batches 0 --cpu-baseline off ;;
+    profdet) DET="python3 tools/rewalk_probe.py --det --batches 3"
+            step det_probe 300 $DET
+            step det_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/det_trace -o run -- $DET
+            step det_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/det_fetch -o run -- $DET
+            step det_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/det_write -o run -- $DET
+            step det_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/det_tcc -o run -- $DET ;;
     pmcn2v) N2V="python3 bench.py --model node2vec --steps 2 --warmup 1 --rewalk-batches 0 --cpu-baseline off"
             step n2v_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/n2v_trace -o run -- $N2V
             step n2v_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/n2v_fetch -o run -- $N2V

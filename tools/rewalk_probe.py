@@ -22,10 +22,11 @@ def main():
     ap.add_argument("--samples", type=int, default=43_000_000)
     ap.add_argument("--batches", type=int, default=6)
     ap.add_argument("--model", default="deepwalk")
+    ap.add_argument("--det", action="store_true", help="deterministic mode (the reference's experiment default)")
     a = ap.parse_args()
     import dynamicgraphrepresentationlearning_amd as W
     n = 1 << a.scale
-    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, deterministic=False, seed=5,
+    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, deterministic=a.det, seed=5,
                         model=W.NODE2VEC if a.model == "node2vec" else W.DEEPWALK)
     g = W.WharfMH.from_rmat(n, a.samples, 2 * n, seed=2, config=cfg)
     g.generate_initial_random_walks()
