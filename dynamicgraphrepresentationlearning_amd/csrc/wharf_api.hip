@@ -570,16 +570,18 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
             a.lockstep_min = lockstep_min();
             // deterministic mode: suffixes walked once per (round, batch source) and copied
-            // (k_det_suffix + k_rewalk_memo) while the table stays small; WHARF_NO_MEMO=1 (tests)
+            // (k_det_suffix + k_rewalk_chunked<true>) while the table stays small; WHARF_NO_MEMO=1 (tests)
             // re-walks every suffix (k_rewalk_sweep)
             const uint64_t stride4 = (h->L + 3) & ~3ull;
             const char* no_memo = getenv("WHARF_NO_MEMO");
             if (a.det && !a.scan_only && k && !(no_memo && atoi(no_memo)) &&
                 (uint64_t)h->wpv * k * stride4 * 4 <= (256ull << 20)) {
                 h->srcidx.ensure(std::max<uint64_t>(h->n, 1) * 4);
-                h->memo.ensure((uint64_t)h->wpv * k * stride4 * 4);
+                // kMemoPad words before and after the table: k_rewalk_chunked reads whole
+                // chunks around a row (values outside the row are never written)
+                h->memo.ensure(((uint64_t)h->wpv * k * stride4 + 2 * kMemoPad) * 4);
                 launch_src_index(h->runs.as<RunInfo>(), k, h->srcidx.as<uint32_t>(), s);
-                a.memo = h->memo.as<uint32_t>();
+                a.memo = h->memo.as<uint32_t>() + kMemoPad;
                 a.src_idx = h->srcidx.as<uint32_t>();
                 a.runs = h->runs.as<RunInfo>();
                 a.memo_k = k;

@@ -13,6 +13,7 @@ namespace wharf {
 
 enum { kDeepWalk = 0, kNode2Vec = 1 };
 enum { kInitRandom = 0, kInitBurnin = 1, kInitWeight = 2 };
+constexpr uint64_t kMemoPad = 64;   // >= the chunk of k_rewalk_chunked
 
 struct RunInfo {
     uint64_t off, end;   // old row [off, end)
@@ -43,12 +44,13 @@ struct WalkArgs {
     int scan_only;               // re-walk: only find rewalk points (apply_walk_updates=false)
     uint64_t* defer;             // re-walk: walks of sparse waves, {li | p << 56}, count in counters[2]
     uint32_t lockstep_min;       // re-walk: a wave with fewer affected walks defers them to `defer`
-    // deterministic re-walk by suffix table (k_det_suffix + k_rewalk_memo), or memo == null
+    // deterministic re-walk by suffix table (k_det_suffix + k_rewalk_chunked<true>), or memo == null
     uint32_t* memo;              // [wpv][k][memo_stride]: walk from batch source i in round r, new graph
     const uint32_t* src_idx;     // [n]: index of a batch source in the run table (read for sources only)
     const RunInfo* runs;         // the batch's source runs
     uint64_t memo_k;             // sources (runs) in the batch
     uint32_t memo_stride;        // L rounded up to 4 (16-B aligned rows)
+                                 // (the table has kMemoPad readable words on either side)
     uint32_t wpv;
 };
 

@@ -487,7 +487,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
 // again (wharfmh.h:813-840), so its suffix depends only on (r, s): it is the
 // first L-1-p steps of a walk STARTING at s in round r on the new graph.  The
 // rewalk vertex is always a batch source, so k_det_suffix walks the wpv x k
-// suffixes once (k <= 10 k distinct sources per batch) and k_rewalk_memo
+// suffixes once (k <= 10 k distinct sources per batch) and k_rewalk_chunked
 // copies them: the re-walk of ~34 M walks becomes a streaming pass over the
 // walk matrix plus reads of a small, cache-resident table, instead of one
 // random graph gather per re-walked position.  Same values, same step count.
@@ -514,62 +514,161 @@ __global__ __launch_bounds__(256) void k_det_suffix(WalkArgs a)
     }
 }
 
-// The sweep of k_rewalk_sweep (lock-step positions, full-row stores), with
-// the walking lanes reading their suffix row four positions per 16-B load.
-// XCD-aware: workgroups are placed on the 8 XCDs round-robin, so XCD x
-// (blockIdx % 8) takes the x-th eighth of the walks — ~1.25 rounds — and its
-// 4 MiB L2 holds the suffix rows of those rounds (k x L x 4 B = 3.2 MB per
-// round at 10 k sources) instead of all of them.
-__global__ __launch_bounds__(256) void k_rewalk_memo(WalkArgs a)
+// Chunked rewalk-point scan (and the suffix-table copy of the deterministic
+// re-walk).  The sweeps above read a lane's old walk one position at a time
+// with one row prefetched: a wave has one 256-B row in flight, so the scan is
+// latency-bound (configs[2]: 6.7 GB in 5.4 ms, 1.2 TB/s).  Here a wave reads
+// kScanChunk rows per round trip: the next chunk's rows are loaded while the
+// current one is tested (Bloom filter in LDS, then the exact bitmap for the
+// positives in ascending order), and in the copy the chunk's rows are
+// written whole — the suffix-table value for walking lanes, the old value
+// (still in registers) for the others.
+#ifndef WHARF_SCAN_CHUNK
+#define WHARF_SCAN_CHUNK 16
+#endif
+#ifndef WHARF_CHUNK_NT
+#define WHARF_CHUNK_NT 3   // bit 0: non-temporal walk loads, bit 1: stores (A/B: -2..-3 % on the copy)
+#endif
+constexpr uint32_t kScanChunk = WHARF_SCAN_CHUNK;
+__device__ __forceinline__ uint32_t walk_load(const uint32_t* p)
 {
+    if (WHARF_CHUNK_NT & 1) return __builtin_nontemporal_load(p);
+    return *p;
+}
+__device__ __forceinline__ void walk_store(uint32_t* p, uint32_t v)
+{
+    if (WHARF_CHUNK_NT & 2) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+static_assert(kMemoPad >= kScanChunk, "suffix table padding");
+static_assert(kScanChunk % 4 == 0 && kScanChunk <= 32, "chunk positions live in a 32-bit mask");
+
+__device__ __forceinline__ uint32_t chunk_pick(const uint32_t (&x)[kScanChunk], uint32_t j)
+{
+    // and/or, not a select chain: LLVM folds selects over an array into a
+    // dynamically indexed load, which puts the array in scratch memory
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kScanChunk; i++) v |= x[i] & (0u - (uint32_t)(j == i));
+    return v;
+}
+
+// First batch source among x[0..cnt) before the old walk's end, or kScanChunk
+// (then `ended` tells whether the walk ended inside the chunk).
+__device__ __forceinline__ uint32_t scan_chunk(const WalkArgs& a, const uint32_t* s_bloom,
+                                               const uint32_t (&x)[kScanChunk], uint32_t cnt, bool& ended)
+{
+    uint32_t mask = 0, end = cnt;
+#pragma unroll
+    for (uint32_t j = 0; j < kScanChunk; j++) {
+        const uint32_t h = bloom_hash(x[j]), h2 = bloom_hash2(x[j]);
+        mask |= ((s_bloom[h >> 5] >> (h & 31)) & (s_bloom[h2 >> 5] >> (h2 & 31)) & 1u) << j;
+        if (x[j] == kSent && j < end) end = j;
+    }
+    if (end < 32) mask &= (1u << end) - 1u;
+    while (mask) {
+        const uint32_t j = (uint32_t)__builtin_ctz(mask);
+        const uint32_t v = chunk_pick(x, j);
+        if ((a.bitmap[v >> 5] >> (v & 31)) & 1u) return j;
+        mask &= mask - 1u;
+    }
+    ended = end < cnt;
+    return kScanChunk;
+}
+
+// XCD-aware walk ranges: workgroup b runs on XCD b % 8, which takes the
+// (b % 8)-th eighth of the walks (whole 256-walk blocks, so rows stay aligned).
+struct XcdRange {
+    uint64_t first, end, stride;
+};
+__device__ __forceinline__ XcdRange xcd_range(uint64_t W)
+{
+    const uint32_t xcd = blockIdx.x % kXcds, slot = blockIdx.x / kXcds, per = gridDim.x / kXcds;
+    const uint64_t part = (((W + kXcds - 1) / kXcds) + 255) & ~255ull;
+    const uint64_t c0 = min(W, (uint64_t)xcd * part);
+    return {c0 + (uint64_t)slot * blockDim.x + threadIdx.x, min(W, c0 + part), (uint64_t)per * blockDim.x};
+}
+
+// COPY = false: rewalk points only (apply_walk_updates = false, any model).
+// COPY = true: deterministic re-walk from the suffix table (k_det_suffix).
+template <bool COPY>
+__global__ __launch_bounds__(256) void k_rewalk_chunked(WalkArgs a)
+{
+    constexpr uint32_t C = kScanChunk;
     __shared__ uint32_t s_bloom[kBloomWords];
     bloom_to_lds(a, s_bloom);
     uint32_t steps = 0;
     uint32_t* __restrict__ walks = a.walks;
     const uint64_t W = a.W;
     const uint32_t L = a.L;
-    const uint32_t xcd = blockIdx.x % kXcds, slot = blockIdx.x / kXcds, per = gridDim.x / kXcds;
-    const uint64_t chunk = (W + kXcds - 1) / kXcds;
-    const uint64_t c0 = xcd * chunk, c1 = min(W, c0 + chunk);
-    const uint64_t stride = (uint64_t)per * blockDim.x;
-    for (uint64_t li = c0 + (uint64_t)slot * blockDim.x + threadIdx.x; li < c1; li += stride) {
+    const XcdRange xr = xcd_range(W);
+    for (uint64_t li = xr.first; li < xr.end; li += xr.stride) {
         const uint64_t r = li / a.n_loc;
-        const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
-        uint32_t mode = kLaneScan, p = kNoRewalk;
-        uint32_t x = v;
-        uint32_t xn = L > 1 ? walks[W + li] : kSent;   // old value at pos + 1 (prefetched)
-        const uint32_t* __restrict__ row = nullptr;
-        uint4 q = make_uint4(kSent, kSent, kSent, kSent);
-        for (uint32_t pos = 0; pos < L; pos++) {
-            uint32_t val = kSent;
-            bool fresh = false;
-            if (mode == kLaneWalk) {
-                const uint32_t j = pos - p;
-                if ((j & 3) == 0 || j == 1) q = *reinterpret_cast<const uint4*>(row + (j & ~3u));
-                const uint32_t e = j & 3;
-                val = e == 0 ? q.x : (e == 1 ? q.y : (e == 2 ? q.z : q.w));
-                steps += val != kSent;
-                fresh = true;
-            } else if (mode == kLaneScan) {
-                if (pos > 0) {
-                    x = xn;
-                    if (pos + 1 < L && x != kSent) xn = walks[(uint64_t)(pos + 1) * W + li];
-                }
-                val = x;
-                if (x == kSent) {
-                    mode = kLaneDone;
-                } else if (is_source(a, s_bloom, x)) {
-                    p = pos;
-                    mode = kLaneWalk;
-                    row = a.memo + (r * a.memo_k + a.src_idx[x]) * a.memo_stride;
+        uint32_t p = kNoRewalk;
+        bool scanning = true;
+        const uint32_t* __restrict__ row = nullptr;   // suffix row shifted by -p: the new value at pos is row[pos]
+        uint32_t cur[C], nxt[C];
+#pragma unroll
+        for (uint32_t j = 0; j < C; j++) cur[j] = j < L ? walk_load(walks + (uint64_t)j * W + li) : kSent;
+        for (uint32_t c0 = 0; c0 < L; c0 += C) {
+            const uint32_t cnt = min(C, L - c0);
+            const bool was_scanning = scanning;
+            if (scanning) {
+                bool ended = false;
+                const uint32_t j = scan_chunk(a, s_bloom, cur, cnt, ended);
+                if (j < C) {
+                    p = c0 + j;
+                    scanning = false;
+                    if (COPY) {
+                        const uint32_t x = chunk_pick(cur, j);
+                        row = a.memo + (r * a.memo_k + a.src_idx[x]) * a.memo_stride - p;
+                    }
+                } else if (ended) {
+                    scanning = false;
                 }
             }
-            if (__any(fresh)) walks[(uint64_t)pos * W + li] = val;
-            if (!__any(mode != kLaneDone)) break;
+            uint32_t mv[C];
+            if (COPY) {
+                const bool walking = p < c0 + cnt - 1;   // new values inside this chunk
+                if (walking) {
+#pragma unroll
+                    for (uint32_t q = 0; q < C; q += 4) {
+                        uint4 t;
+                        __builtin_memcpy(&t, row + c0 + q, 16);
+                        mv[q] = t.x, mv[q + 1] = t.y, mv[q + 2] = t.z, mv[q + 3] = t.w;
+                    }
+                }
+            }
+            // next chunk's rows, in flight while this chunk is written
+            const bool more = c0 + C < L;
+            if (more && scanning) {
+#pragma unroll
+                for (uint32_t j = 0; j < C; j++)
+                    nxt[j] = c0 + C + j < L ? walk_load(walks + (uint64_t)(c0 + C + j) * W + li) : kSent;
+            }
+            if (COPY) {
+#pragma unroll
+                for (uint32_t j = 0; j < C; j++) {
+                    const uint32_t pos = c0 + j;
+                    if (j < cnt && __any(p < pos)) {
+                        uint32_t val = was_scanning ? cur[j] : kSent;
+                        if (p < pos) {
+                            val = mv[j];
+                            steps += val != kSent;
+                        }
+                        walk_store(walks + (uint64_t)pos * W + li, val);
+                    }
+                }
+            }
+            if (!__any(scanning || (COPY && p != kNoRewalk))) break;
+            if (more && scanning) {
+#pragma unroll
+                for (uint32_t j = 0; j < C; j++) cur[j] = nxt[j];
+            }
         }
         a.aff[li] = (uint8_t)p;
     }
-    wave_add(a.counters + 0, steps);
+    if (COPY) wave_add(a.counters + 0, steps);
 }
 
 __global__ void k_src_index(const RunInfo* __restrict__ runs, uint64_t k, uint32_t* __restrict__ src_idx)
@@ -771,11 +870,17 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
             hipLaunchKernelGGL((k_walk<M, D>), grid, block, 0, s, a);                        \
         }                                                                                    \
     } while (0)
+    // a multiple of 8 workgroups: every XCD gets the same number
+    const dim3 mgrid((std::max<unsigned>(grid.x, kXcds) / kXcds) * kXcds);
+    const char* nc = getenv("WHARF_NO_CHUNKED_SCAN");   // A/B and tests: scan-only by the sweeps
+    const bool chunked = !(nc && atoi(nc));
     if (rewalk && a.det && a.memo && !a.scan_only) {
         hipLaunchKernelGGL(k_det_suffix, grid_for((uint64_t)a.wpv * a.memo_k, 256), 256, 0, s, a);
-        // a multiple of 8 workgroups: every XCD gets the same number
-        const dim3 mgrid((std::max<unsigned>(grid.x, kXcds) / kXcds) * kXcds);
-        hipLaunchKernelGGL(k_rewalk_memo, mgrid, block, 0, s, a);
+        hipLaunchKernelGGL(k_rewalk_chunked<true>, mgrid, block, 0, s, a);
+        return;
+    }
+    if (rewalk && a.scan_only && chunked) {
+        hipLaunchKernelGGL(k_rewalk_chunked<false>, mgrid, block, 0, s, a);
         return;
     }
     if (a.det) WHARF_LAUNCH(kDeepWalk, true);

@@ -306,9 +306,10 @@ def test_affected_ids_on_device_match_host_list(W):
     gd.destroy()
 
 
-# (WHARF_LOCKSTEP_MIN, WHARF_MOVE_NO_LDS, WHARF_FORCE_RECORD_REBUILD, neighbour filter, WHARF_NO_MEMO)
-PATHS = {"sweep/patch-lds": ("0", "0", "0", "on", "1"), "deferred/inplace-l2": ("65", "1", "1", "noslack", "0"),
-         "mixed/inplace-lds": ("40", "0", "1", "off", "0"), "mixed/gather": ("16", "1", "2", "on", "1")}
+# (WHARF_LOCKSTEP_MIN, WHARF_MOVE_NO_LDS, WHARF_FORCE_RECORD_REBUILD, neighbour filter, WHARF_NO_MEMO,
+#  WHARF_NO_CHUNKED_SCAN)
+PATHS = {"sweep/patch-lds": ("0", "0", "0", "on", "1", "0"), "deferred/inplace-l2": ("65", "1", "1", "noslack", "0", "0"),
+         "mixed/inplace-lds": ("40", "0", "1", "off", "0", "1"), "mixed/gather": ("16", "1", "2", "on", "1", "1")}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -324,10 +325,13 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     anchors kept aside (WHARF_FORCE_RECORD_REBUILD=1 / 2).  node2vec anchor
     inits with the per-row neighbour filters (re-filled per source row, or with
     no pool headroom re-built whole whenever a row outgrows its words) and
-    without them.  Deterministic re-walks by suffix table (k_rewalk_memo) and
-    by walking every suffix (WHARF_NO_MEMO=1, k_rewalk_sweep)."""
-    lockstep_min, no_lds, force, filt, no_memo = PATHS[path]
+    without them.  Deterministic re-walks by suffix table (k_rewalk_chunked
+    copy) and by walking every suffix (WHARF_NO_MEMO=1, k_rewalk_sweep).
+    Rewalk points alone (apply_walk_updates = false): the chunked scan, or
+    with WHARF_NO_CHUNKED_SCAN=1 the sweep kernels in scan-only mode."""
+    lockstep_min, no_lds, force, filt, no_memo, no_chunked = PATHS[path]
     monkeypatch.setenv("WHARF_NO_MEMO", no_memo)
+    monkeypatch.setenv("WHARF_NO_CHUNKED_SCAN", no_chunked)
     monkeypatch.setenv("WHARF_NO_NEIGHBOUR_FILTER", "1" if filt == "off" else "0")
     monkeypatch.setenv("WHARF_FILTER_NO_SLACK", "1" if filt == "noslack" else "0")
     monkeypatch.setenv("WHARF_LOCKSTEP_MIN", lockstep_min)
@@ -337,6 +341,7 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     off, adj = O.csr_from_edges(1 << 12, base)
     batches = [(True, O.generate_batch_of_edges(800, 1 << 12, 11, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
                (False, O.generate_batch_of_edges(600, 1 << 12, 12, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
+               (True, O.generate_batch_of_edges(500, 1 << 12, 14, False, False), O.REMOVE_DUPS),   # rewalk points only
                (True, O.generate_batch_of_edges(40, 1 << 12, 13, False, True), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES)]
     kw = dict(deterministic=True) if mode == "det" else dict(
         deterministic=False, seed=99, model=1 if mode == "node2vec" else 0, paramP=0.5, paramQ=2.0)

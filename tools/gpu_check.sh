@@ -39,6 +39,14 @@ for s in "$@"; do
     c4)     step c4_stream 1100 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 50 ;;
     c5n2v)  step c5_node2vec 1100 python tools/bigscale.py --model node2vec --wpv 1 --batches 10 --mixed ;;
     detnm)  step bench_det_nomemo 900 env WHARF_NO_MEMO=1 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
+    chunk)  step probe_det 300 python tools/rewalk_probe.py --det --batches 3
+            step probe_det_nochunk 300 env WHARF_NO_CHUNKED_SCAN=1 python tools/rewalk_probe.py --det --batches 3
+            step probe_mh 300 python tools/rewalk_probe.py --batches 3
+            step probe_mh_nochunk 300 env WHARF_NO_CHUNKED_SCAN=1 python tools/rewalk_probe.py --batches 3 ;;
+    ab)     for v in cur ${AB:-$(ls tools/ab 2>/dev/null | sed -n 's/^lib_\(.*\)\.so$/\1/p')}; do
+              lib=""; [ $v = cur ] || lib=tools/ab/lib_$v.so
+              step ab_det_$v 300 env WHARF_LIB_PATH=$lib python tools/rewalk_probe.py --det --batches 3
+            done ;;
     det)    step bench_det 900 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     n2vnf)  step bench_n2v_nofilter 900 env WHARF_NO_NEIGHBOUR_FILTER=1 python bench.py --model node2vec --steps 2 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     c5n2vnf) step c5_node2vec_nofilter 1100 env WHARF_NO_NEIGHBOUR_FILTER=1 python tools/bigscale.py --model node2vec --wpv 1 --batches 4 --mixed --no-oracle ;;
