@@ -8,6 +8,16 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+# One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 and its
+# libraries ask for it as "libamdhip64.so"; libwharf_gpu.so asks for the soname
+# "libamdhip64.so.7".  Loaded torch-first, our request resolves to torch's
+# runtime; loaded the other way round the process would map two HIP/HSA
+# runtimes and torch's would find no GPU ("No HIP GPUs are available").
+try:
+    import torch  # noqa: F401
+except ImportError:   # torch is plumbing (device buffers, streams, torch.distributed), not required
+    pass
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # WHARF_LIB_PATH: an alternative build of the same library (A/B experiments in tools/)
 LIB_PATH = os.environ.get("WHARF_LIB_PATH") or os.path.join(_HERE, "libwharf_gpu.so")

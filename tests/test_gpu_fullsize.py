@@ -11,7 +11,10 @@ bit for bit and the rest is checked structurally:
   ids are exactly the walks holding a batch source (ascending), every position
   up to a walk's rewalk point is unchanged, unaffected walks are unchanged,
   re-walked transitions are edges of the new graph, and the step counter equals
-  the number of re-walked transitions.
+  the number of re-walked transitions;
+
+  the same batch in deterministic mode: every re-walked suffix equals the walk
+  of its round from its batch source on the new graph.
 """
 import numpy as np
 import pytest
@@ -114,3 +117,50 @@ def test_configs2_full_size_insert_batch(W, torch):
             assert _all_edges(torch, ekeys, n, after[pos, m], after[pos + 1, m]), f"non-edge re-walk step at {pos}"
     assert walked == steps
     g.destroy()
+
+
+def test_configs2_full_size_deterministic_batch(W, torch):
+    """Deterministic mode at configs[2] size (the suffix table + chunked copy):
+    every affected walk's new suffix from its rewalk point p at batch source s
+    equals the first L - p positions of round r's walk STARTING at s on the new
+    graph (the reference restarts Random(r) at draw 0, wharfmh.h:813-840) —
+    checked for all ~34 M affected walks against a fresh device generation
+    (k_walk, bit-exact against the oracle elsewhere); positions up to p and
+    unaffected walks are unchanged; the step counter matches."""
+    n = 1 << 22
+    sent = int(np.uint32(W.SENTINEL).view(np.int32))
+    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=L, deterministic=True)
+    g = W.WharfMH.from_rmat(n, 43_000_000, 2 * n, seed=3, config=cfg)
+    g.generate_initial_random_walks()
+    before = _dev_walks(torch, g)
+    batch = W.generate_batch_of_edges(5000, n, 0, False, False)
+    ids = torch.empty(g.number_of_walks, dtype=torch.int32, device="cuda:0")
+    aff = g.insert_edges_batch(batch, remove_dups=True, out=ids)
+    steps = g.stats()["steps"]
+    after = _dev_walks(torch, g)
+    g.generate_initial_random_walks()        # round-r walks from every vertex on the new graph
+    fresh = _dev_walks(torch, g)
+    g.destroy()
+    is_src = torch.zeros(n, dtype=torch.bool, device="cuda:0")
+    is_src[torch.from_numpy(batch[:, 0].astype(np.int64)).cuda()] = True
+    Wn = before.shape[1]
+    p = torch.full((Wn,), L, dtype=torch.int64, device="cuda:0")
+    for pos in range(L - 1, -1, -1):
+        row = before[pos]
+        hit = (row != sent) & is_src[row.clamp(min=0).long()]
+        p = torch.where(hit, torch.full_like(p, pos), p)
+    affected = p < L
+    assert torch.equal(aff.long(), torch.nonzero(affected).squeeze(1))
+    cols = torch.arange(Wn, device="cuda:0")
+    pa = p.clamp(max=L - 1)
+    s = before[pa, cols].long()                              # the batch source at the rewalk point
+    start = (cols // n) * n + s                              # walk id of round r from s
+    walked = 0
+    for pos in range(L):
+        kept = pos <= p
+        assert torch.equal(after[pos][kept], before[pos][kept]), f"position {pos} changed before the rewalk point"
+        m = affected & (pos > p)
+        exp = fresh[(pos - pa)[m], start[m]]
+        assert torch.equal(after[pos][m], exp), f"re-walked suffix differs from the walk from its source at {pos}"
+        walked += int((after[pos][m] != sent).sum())
+    assert walked == steps
