@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--paramQ", type=float, default=2.0)
     p.add_argument("--det", action="store_true", help="deterministic mode instead of MH")
     p.add_argument("--rewalk-batches", type=int, default=50, help="10k-edge insert batches (configs[2])")
+    p.add_argument("--det-rewalk-batches", type=int, default=10,
+                   help="the same stream in deterministic mode (DeepWalk MH runs only; 0 = off)")
     p.add_argument("--stream-samples", type=int, default=43_000_000, help="configs[2] base graph undirected samples")
     p.add_argument("--cpu-baseline", choices=["auto", "reference", "port", "off"], default="auto")
     p.add_argument("--cpu-threads", type=int, default=0)
@@ -169,6 +171,69 @@ def cpu_baseline(args, n, active_vertices, off, adj, kind):
                       f"{steps} steps in {secs:.2f} s", "seconds": secs}
 
 
+def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrier, batches):
+    """configs[2]: per-batch latency of 10k-edge insert batches with the re-walk applied
+    (memory-throughput-latency.cpp:126-134: generate_batch_of_edges(5000, n, seed=b, false, undirected))."""
+    if batches <= 0:
+        return None
+    ns = 1 << args.scale   # configs[2] is a one-GPU graph: not grown with the ranks
+    gs = W.WharfMH.from_rmat(ns, args.stream_samples, 2 * ns, seed=args.seed + 1, config=cfg, device=dev)
+    gs.set_shard(*balanced_shards(np.diff(gs.offsets().astype(np.int64)), world)[rank])
+    gs.generate_initial_random_walks()
+    gs.generate_initial_random_walks()
+    s1 = gs.stats()
+    gen3 = {"ms": round(s1["last_walk_kernel_ms"], 3), "steps": s1["steps"]}
+    # affected walk ids stay in HBM (WHARF_AFFECTED_DEVICE); the host-list
+    # variant (PCIe-inclusive, the reference's return value) is timed after
+    out = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
+    lat, aff, gu, wu, kern, rsteps = [], [], [], [], [], []
+    for b in range(batches):
+        batch = W.generate_batch_of_edges(5000, ns, b, False, False, device=dev)
+        barrier()
+        t1 = time.perf_counter()
+        a = gs.insert_edges_batch(batch, remove_dups=True, out=out)
+        barrier()
+        lat.append((time.perf_counter() - t1) * 1e3)
+        s2 = gs.stats()
+        aff.append(len(a))
+        gu.append(s2["last_graph_update_ms"])
+        wu.append(s2["last_walk_update_ms"])
+        kern.append(s2["last_walk_kernel_ms"])
+        rsteps.append(s2["steps"])
+    hout = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, pin_memory=True).numpy().view(np.uint32)
+    lat_host = []
+    for b in range(batches, batches + min(5, batches)):
+        batch = W.generate_batch_of_edges(5000, ns, b, False, False, device=dev)
+        barrier()
+        t1 = time.perf_counter()
+        gs.insert_edges_batch(batch, remove_dups=True, out=hout)
+        barrier()
+        lat_host.append((time.perf_counter() - t1) * 1e3)
+    lat_all = lat
+    if dist:
+        tl = torch.tensor(lat, dtype=torch.float64, device=comm_dev)
+        dist.all_reduce(tl, op=dist.ReduceOp.MAX)
+        lat_all = tl.tolist()
+    res = {"workload": f"configs[2] soc-LiveJournal-sized streaming: RMAT scale {args.scale}, "
+                       f"{args.stream_samples} undirected samples (m={gs.number_of_edges()}), "
+                       f"{batches} insert batches of generate_batch_of_edges(5000, n, b, false, "
+                       f"undirected), re-walk applied",
+           "batches": batches, "edges_per_batch": int(len(batch)),
+           "median_ms": round(float(np.median(lat_all)), 3), "p90_ms": round(float(np.percentile(lat_all, 90)), 3),
+           "median_ms_ids_to_host_pinned": round(float(np.median(lat_host)), 3),
+           "mean_affected_walks_rank0": int(np.mean(aff)),
+           "median_graph_update_ms": round(float(np.median(gu)), 3),
+           "median_walk_update_ms": round(float(np.median(wu)), 3),
+           "median_rewalk_kernel_ms": round(float(np.median(kern)), 3),
+           "mean_rewalk_steps_rank0": int(np.mean(rsteps)),
+           "rewalk_Gsteps_per_s": round(float(np.sum(rsteps) / np.sum(kern) / 1e6), 2),
+           "generation_same_graph": gen3}
+    gs.destroy()
+    return res
+
+
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -265,63 +330,15 @@ def main():
 
     g.destroy()
 
-    # configs[2]: soc-LiveJournal-sized streaming, 10k-edge insert batches
-    # (memory-throughput-latency.cpp:126-134: generate_batch_of_edges(5000, n, seed=b, false, undirected))
-    rewalk = None
-    if args.rewalk_batches > 0:
-        ns = 1 << args.scale   # configs[2] is a one-GPU graph: not grown with the ranks
-        gs = W.WharfMH.from_rmat(ns, args.stream_samples, 2 * ns, seed=args.seed + 1, config=cfg, device=dev)
-        gs.set_shard(*balanced_shards(np.diff(gs.offsets().astype(np.int64)), world)[rank])
-        gs.generate_initial_random_walks()
-        gs.generate_initial_random_walks()
-        s1 = gs.stats()
-        gen3 = {"ms": round(s1["last_walk_kernel_ms"], 3), "steps": s1["steps"]}
-        # affected walk ids stay in HBM (WHARF_AFFECTED_DEVICE); the host-list
-        # variant (PCIe-inclusive, the reference's return value) is timed after
-        out = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
-        lat, aff, gu, wu, kern, rsteps = [], [], [], [], [], []
-        for b in range(args.rewalk_batches):
-            batch = W.generate_batch_of_edges(5000, ns, b, False, False, device=dev)
-            barrier()
-            t1 = time.perf_counter()
-            a = gs.insert_edges_batch(batch, remove_dups=True, out=out)
-            barrier()
-            lat.append((time.perf_counter() - t1) * 1e3)
-            s2 = gs.stats()
-            aff.append(len(a))
-            gu.append(s2["last_graph_update_ms"])
-            wu.append(s2["last_walk_update_ms"])
-            kern.append(s2["last_walk_kernel_ms"])
-            rsteps.append(s2["steps"])
-        hout = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, pin_memory=True).numpy().view(np.uint32)
-        lat_host = []
-        for b in range(args.rewalk_batches, args.rewalk_batches + min(5, args.rewalk_batches)):
-            batch = W.generate_batch_of_edges(5000, ns, b, False, False, device=dev)
-            barrier()
-            t1 = time.perf_counter()
-            gs.insert_edges_batch(batch, remove_dups=True, out=hout)
-            barrier()
-            lat_host.append((time.perf_counter() - t1) * 1e3)
-        lat_all = lat
-        if dist:
-            tl = torch.tensor(lat, dtype=torch.float64, device=comm_dev)
-            dist.all_reduce(tl, op=dist.ReduceOp.MAX)
-            lat_all = tl.tolist()
-        rewalk = {"workload": f"configs[2] soc-LiveJournal-sized streaming: RMAT scale {args.scale}, "
-                              f"{args.stream_samples} undirected samples (m={gs.number_of_edges()}), "
-                              f"{args.rewalk_batches} insert batches of generate_batch_of_edges(5000, n, b, false, "
-                              f"undirected), re-walk applied",
-                  "batches": args.rewalk_batches, "edges_per_batch": int(len(batch)),
-                  "median_ms": round(float(np.median(lat_all)), 3), "p90_ms": round(float(np.percentile(lat_all, 90)), 3),
-                  "median_ms_ids_to_host_pinned": round(float(np.median(lat_host)), 3),
-                  "mean_affected_walks_rank0": int(np.mean(aff)),
-                  "median_graph_update_ms": round(float(np.median(gu)), 3),
-                  "median_walk_update_ms": round(float(np.median(wu)), 3),
-                  "median_rewalk_kernel_ms": round(float(np.median(kern)), 3),
-                  "mean_rewalk_steps_rank0": int(np.mean(rsteps)),
-                  "rewalk_Gsteps_per_s": round(float(np.sum(rsteps) / np.sum(kern) / 1e6), 2),
-                  "generation_same_graph": gen3}
-        gs.destroy()
+    # configs[2]: soc-LiveJournal-sized streaming, 10k-edge insert batches, in the
+    # benchmarked mode and (DeepWalk MH runs) in deterministic mode, the reference's default
+    rewalk = stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrier, args.rewalk_batches)
+    rewalk_det = None
+    if args.det_rewalk_batches > 0 and not args.det and args.model == "deepwalk":
+        cfg_det = W.WharfConfig(walks_per_vertex=args.wpv, walk_length=args.length, model=W.DEEPWALK,
+                                deterministic=True)
+        rewalk_det = stream_latency(args, W, torch, cfg_det, dev, world, rank, dist, comm_dev, barrier,
+                                    args.det_rewalk_batches)
 
     if rank == 0:
         live_ceiling = measure_gather_ceiling() if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None
@@ -361,6 +378,7 @@ def main():
                          if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None},
             "mh_accept_rate": round(st["accepts"] / st["steps"], 5) if st["steps"] else None,
             "rewalk_latency_10k_batch": rewalk,
+            "rewalk_latency_10k_batch_deterministic": rewalk_det,
             "corpus_allgatherv": corpus,
             "cpu_baseline": None,
         }
