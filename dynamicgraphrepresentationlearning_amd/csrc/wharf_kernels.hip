@@ -227,14 +227,18 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
 // SamplerManager::find (a copy, so the anchor stays frozen: libcuckoo find()
 // returns by value, cuckoohash_map.hh:596-609).  The anchor of state
 // (cur, prev) is cached on the edge prev->cur the walker just crossed (`ein`,
-// its global CSR slot, or -1), tagged with the epoch it was computed in; it
-// stays valid while neither row changed since (samplers of batch sources are
-// reset, wharfmh.h:504,539).  Every writer of an entry writes the same value,
-// a pure function of the current snapshot, so lazy races are benign and the
-// result does not depend on which walks (or which GPU) touched it first.
-// The entry also keeps the anchor's weight class (it depends only on (prev,
-// anchor) and prev's row, which the tag covers), so an accepted step needs one
-// has_edge, not two.  Entry = slot | tag << 32 | class << 62.
+// its global CSR slot, or -1), tagged with the epoch it was written in.  The
+// reference keeps the sampler in cur's SamplerManager (wharfmh.h:296-301),
+// which is reset only when cur is a batch source (wharfmh.h:504,539): the
+// anchor stays valid while cur's row is unchanged since the tag.  Every
+// writer of an entry writes the same value, a pure function of the current
+// snapshot, so lazy races are benign and the result does not depend on which
+// walks (or which GPU) touched it first.
+// The entry also keeps the anchor's weight class, so an accepted step needs
+// one has_edge, not two.  The class depends on prev's row (node2vec.h:74-88
+// evaluates has_edge(prev, anchor) on the current graph at every sample()):
+// when prev was a batch source since the tag, the anchor stands and only its
+// class is re-evaluated and re-tagged.  Entry = slot | tag << 32 | class << 62.
 //
 // node2vec MH keeps the entry of slot e inside e's 32-B edge record (bytes
 // 16-23), so the gather that crosses an edge also brings the anchor of the
@@ -244,9 +248,15 @@ __device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc,
 {
     if (ein >= 0) {
         const uint32_t tag = (uint32_t)(anc >> 32) & 0x3FFFFFFFu;
-        if (anc != kAnchorNone64 && tag >= rc.epoch && tag >= rp.epoch) {
-            cls = (uint32_t)(anc >> 62);
-            return (uint32_t)anc;
+        if (anc != kAnchorNone64 && tag >= rc.epoch) {
+            const uint32_t an = (uint32_t)anc;
+            if (tag >= rp.epoch) {
+                cls = (uint32_t)(anc >> 62);
+            } else {
+                cls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + an]);
+                a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+            }
+            return an;
         }
     }
     const uint32_t an = anchor_init(a, rc, rp, cls);

@@ -282,14 +282,16 @@ static uint32_t anchor_init(const wo_engine* e, uint32_t cur, uint32_t prev)
 
 /* SamplerManager::find returns a copy (libcuckoo find(), cuckoohash_map.hh:596-609),
  * so a state's anchor stays frozen.  Cached on the edge prev -> cur (`ein`,
- * its CSR slot, or -1) with the epoch it was computed in; valid while neither
- * row was reset since (samplers of batch sources are reset, wharfmh.h:504,539). */
+ * its CSR slot, or -1) with the epoch it was computed in; the sampler lives in
+ * cur's SamplerManager (wharfmh.h:296-301), so it stays valid while cur's row
+ * was not reset since (samplers of batch sources are reset, wharfmh.h:504,539);
+ * its weight is re-evaluated on the current graph at every sample(). */
 static uint32_t anchor_get(wo_engine* e, uint32_t cur, uint32_t prev, int64_t ein)
 {
     if (ein < 0) return anchor_init(e, cur, prev);
     uint64_t a = __atomic_load_n(&e->anchor[ein], __ATOMIC_RELAXED);
     uint32_t tag = (uint32_t)(a >> 32);
-    if (a != ANCHOR_NONE && tag >= e->row_epoch[cur] && tag >= e->row_epoch[prev]) return (uint32_t)a;
+    if (a != ANCHOR_NONE && tag >= e->row_epoch[cur]) return (uint32_t)a;
     uint32_t s = anchor_init(e, cur, prev);
     __atomic_store_n(&e->anchor[ein], ((uint64_t)e->epoch << 32) | s, __ATOMIC_RELAXED);
     return s;

@@ -23,11 +23,15 @@ def main():
     ap.add_argument("--batches", type=int, default=6)
     ap.add_argument("--model", default="deepwalk")
     ap.add_argument("--det", action="store_true", help="deterministic mode (the reference's experiment default)")
+    ap.add_argument("--init", choices=["random", "burnin", "weight"], default="weight", help="MH sampler init")
+    ap.add_argument("--p", type=float, default=0.5)
+    ap.add_argument("--q", type=float, default=2.0)
     a = ap.parse_args()
     import dynamicgraphrepresentationlearning_amd as W
     n = 1 << a.scale
     cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, deterministic=a.det, seed=5,
-                        model=W.NODE2VEC if a.model == "node2vec" else W.DEEPWALK)
+                        model=W.NODE2VEC if a.model == "node2vec" else W.DEEPWALK, paramP=a.p, paramQ=a.q,
+                        sampler_init={"random": W.RANDOM, "burnin": W.BURNIN, "weight": W.WEIGHT}[a.init])
     g = W.WharfMH.from_rmat(n, a.samples, 2 * n, seed=2, config=cfg)
     g.generate_initial_random_walks()
     res = {"scan_only_ms": [], "fused_ms": [], "affected": [], "steps": []}
