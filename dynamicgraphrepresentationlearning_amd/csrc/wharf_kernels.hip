@@ -123,78 +123,15 @@ __device__ __forceinline__ float weight(const WalkArgs& a, const Row& rprev, uin
 }
 
 // MetropolisHastingsSampler::init (metropolis_hastings_sampler.h:69-108) with
-// proposals from the (cur, prev, epoch of cur's row) Philox stream.  Returns
-// the anchor as a slot of cur's row, and its weight class.
-//
-// WEIGHT (best of 1 + 20 proposals, strict '>', so the first maximum wins):
-// the proposals' targets are loaded in groups of independent reads, and
-// has_edge is asked only while it can matter: once the best weight reaches
-// max(1, 1/q) only a return proposal (c == prev, no lookup) can beat it, and
-// with q == 1 triangle and outward weigh the same.  Same result as the
-// sequential loop.  (configs[4] node2vec re-walks init an anchor every 4th
-// step, with ~18 has_edge calls each: triangle and return proposals are rare
-// on RMAT graphs.  Scanning all proposals for a return first, which needs no
-// lookup, cost more than it saved: 151 -> 185 ms.)
-#ifndef WHARF_PROPOSAL_GROUP
-#define WHARF_PROPOSAL_GROUP 4
-#endif
-constexpr uint32_t kWeightProposals = 21, kProposalGroup = WHARF_PROPOSAL_GROUP;
+// proposals from the (cur, prev, epoch of cur's row) Philox stream: RANDOM
+// and BURNIN, one lane at a time.  Returns the anchor as a slot of cur's row,
+// and its weight class.  WEIGHT (best of 1 + 20 proposals) is evaluated by
+// the whole wave: anchor_init_wave below.
+constexpr uint32_t kWeightProposals = 21;
 
 __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp, uint32_t& cls)
 {
     const uint32_t ep = rc.epoch << 4;
-    if (a.init == kInitWeight) {
-        const float wtop = fmaxf(1.0f, a.inv_q);   // best weight a non-return proposal can have
-        float best = 0.0f;
-        uint32_t last = 0, lcls = 2;
-        const bool use_f = a.fpool && a.inv_q != 1.0f;   // prev's neighbour filter
-        const uint64_t fd = use_f ? a.fdir[rp.v] : 0;
-        for (uint32_t g = 0; g < kWeightProposals; g += kProposalGroup) {
-            uint32_t slot[kProposalGroup], cv[kProposalGroup];
-#pragma unroll
-            for (uint32_t k = 0; k < kProposalGroup; k++) {
-                const uint32_t j = g + k < kWeightProposals ? g + k : kWeightProposals - 1;
-                const P4 r = philox4x32_10(rc.v, rp.v, j, ep | kStreamAnchor, a.key0, a.key1);
-                slot[k] = (uint32_t)pick32(r.x0, rc.deg);
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < kProposalGroup; k++) cv[k] = a.adj[rc.off + slot[k]];
-            // the group's filter words in one round of independent loads (skipped once
-            // only a return proposal can still win)
-            uint32_t maybe = (1u << kProposalGroup) - 1;
-            if (use_f && !(g > 0 && best >= wtop)) {
-                uint32_t fw[kProposalGroup], fb[kProposalGroup];
-#pragma unroll
-                for (uint32_t k = 0; k < kProposalGroup; k++) {
-                    const uint64_t h = filt_hash(cv[k]);
-                    fb[k] = filt_bits(h);
-                    fw[k] = a.fpool[filt_word(fd, h)];
-                }
-                maybe = 0;
-#pragma unroll
-                for (uint32_t k = 0; k < kProposalGroup; k++) maybe |= (uint32_t)((fw[k] & fb[k]) == fb[k]) << k;
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < kProposalGroup; k++) {
-                const uint32_t j = g + k;
-                if (j >= kWeightProposals) break;
-                uint32_t c;
-                if (cv[k] == rp.v) {
-                    c = 0;
-                } else {
-                    if (j > 0 && best >= wtop) continue;   // cannot be strictly greater
-                    // q == 1: triangle and outward weigh the same, the class cannot matter;
-                    // a filter negative is exact (no false negatives)
-                    c = a.inv_q == 1.0f || ((maybe >> k) & 1u) == 0 ? (a.inv_q == 1.0f ? 1u : 2u)
-                                                                    : (has_edge(a, rp, cv[k]) ? 1u : 2u);
-                }
-                const float w = class_weight(a, c);
-                if (j == 0 || w > best) { best = w; last = slot[k]; lcls = c; }
-            }
-        }
-        cls = lcls;
-        return last;
-    }
     P4 r = philox4x32_10(rc.v, rp.v, 0, ep | kStreamAnchor, a.key0, a.key1);
     uint32_t last = (uint32_t)pick32(r.x0, rc.deg);
     uint32_t lcls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + last]);
@@ -243,24 +180,155 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
 // node2vec MH keeps the entry of slot e inside e's 32-B edge record (bytes
 // 16-23), so the gather that crosses an edge also brings the anchor of the
 // state it enters: `anc` is that entry, carried by the walker.
-__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, int64_t ein,
-                                               uint64_t anc, uint32_t& cls)
+//
+// WEIGHT inits are evaluated by the whole wave at once (anchor_init_wave):
+// the lanes that need one publish their (cur, prev) rows, and the wave's 64
+// lanes evaluate the 21 proposals of every such init side by side — targets,
+// then prev's filter words, then has_edge for filter positives, each one
+// round of independent loads for up to kInitRounds proposals per active lane — instead
+// of each lane walking its 21 proposals in dependent groups of 4 while the
+// rest of its (lock-step) wave waits; proposals go to the lanes active at
+// the call, whichever they are (that version: configs[2] node2vec
+// re-walk batch 84 ms, first generation 224 ms).  A per-init LDS minimum over
+// (weight rank, proposal index) keeps the reference's choice: the first
+// proposal of maximal weight (strict '>', metropolis_hastings_sampler.h:84-93).
+// Proposals need no has_edge when q == 1 (triangle and outward weigh the
+// same) or when prev's neighbour filter says no (exact).
+#ifndef WHARF_COOP_FENCE
+#define WHARF_COOP_FENCE 0
+#endif
+#ifndef WHARF_INIT_ROUNDS
+#define WHARF_INIT_ROUNDS 2
+#endif
+constexpr uint32_t kInitRounds = WHARF_INIT_ROUNDS;   // 64-proposal rounds in flight
+constexpr uint32_t kWavesPerBlock = 4;                // every walk kernel runs 256-thread blocks
+
+struct InitReq {     // a lane's init, published for the wave
+    uint32_t cv, cdeg, cep, pv, pdeg;
+    uint64_t coff, poff, fd;
+};
+
+__device__ __forceinline__ uint32_t nth_set_lane(uint64_t mask, uint32_t t)   // lane of the t-th set bit
 {
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t w = 32; w > 0; w >>= 1) {
+        const uint32_t below = (uint32_t)__popcll(mask & ((1ull << (lo + w)) - 1));
+        if (below <= t) lo += w;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+#if WHARF_COOP_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
+    __builtin_amdgcn_wave_barrier();
+#endif
+}
+
+__device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, const Row& rp, uint32_t& slot,
+                                 uint32_t& cls)
+{
+    __shared__ InitReq s_req[kWavesPerBlock][64];
+    __shared__ uint32_t s_key[kWavesPerBlock][64];
+    const uint64_t mask = __ballot(need);
+    if (!mask) return;
+    // proposals are dealt over the lanes active here (the caller's walking lanes), not all 64
+    const uint64_t act = __ballot(1), below = (1ull << __lane_id()) - 1;
+    const uint32_t wv = threadIdx.x >> 6, nact = (uint32_t)__popcll(act), lane = (uint32_t)__popcll(act & below);
+    const uint32_t cnt = (uint32_t)__popcll(mask), me = (uint32_t)__popcll(mask & below);
+    const bool use_f = a.fpool && a.inv_q != 1.0f;
+    if (need) {
+        s_req[wv][me] = InitReq{rc.v, rc.deg, rc.epoch, rp.v, rp.deg, rc.off, rp.off, use_f ? a.fdir[rp.v] : 0ull};
+        s_key[wv][me] = ~0u;
+    }
+    wave_lds_sync();
+    // rank of each class by weight (ties share a rank, so the first proposal wins among them)
+    const float w0 = a.inv_p, w1 = 1.0f, w2 = a.inv_q;
+    const uint32_t rk0 = (w1 > w0) + (w2 > w0), rk1 = (w0 > w1) + (w2 > w1), rk2 = (w0 > w2) + (w1 > w2);
+    const uint32_t total = cnt * kWeightProposals;
+    for (uint32_t base = 0; base < total; base += nact * kInitRounds) {
+        uint32_t t[kInitRounds], j[kInitRounds], cv[kInitRounds], fw[kInitRounds], fb[kInitRounds];
+#pragma unroll
+        for (uint32_t b = 0; b < kInitRounds; b++) {
+            const uint32_t it = base + b * nact + lane;
+            t[b] = it < total ? it / kWeightProposals : cnt;
+            j[b] = it - t[b] * kWeightProposals;
+            cv[b] = 0;
+            if (t[b] < cnt) {
+                const InitReq q = s_req[wv][t[b]];
+                const P4 r = philox4x32_10(q.cv, q.pv, j[b], (q.cep << 4) | kStreamAnchor, a.key0, a.key1);
+                cv[b] = a.adj[q.coff + pick32(r.x0, q.cdeg)];
+            }
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kInitRounds; b++) {
+            fw[b] = 0, fb[b] = 0;
+            if (t[b] < cnt && use_f && cv[b] != s_req[wv][t[b]].pv) {
+                const uint64_t h = filt_hash(cv[b]);
+                fb[b] = filt_bits(h);
+                fw[b] = a.fpool[filt_word(s_req[wv][t[b]].fd, h)];
+            }
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kInitRounds; b++) {
+            if (t[b] >= cnt) continue;
+            const InitReq q = s_req[wv][t[b]];
+            uint32_t c;
+            if (cv[b] == q.pv) c = 0;
+            else if (a.inv_q == 1.0f) c = 1;   // triangle and outward weigh the same
+            else if (use_f && (fw[b] & fb[b]) != fb[b]) c = 2;   // filter negative: exact
+            else c = has_edge(a, Row{q.pv, q.pdeg, 0u, q.poff}, cv[b]) ? 1 : 2;
+            const uint32_t rk = c == 0 ? rk0 : (c == 1 ? rk1 : rk2);
+            atomicMin(&s_key[wv][t[b]], (rk << 7) | (j[b] << 2) | c);
+        }
+    }
+    wave_lds_sync();
+    if (need) {
+        const uint32_t key = s_key[wv][me];
+        const P4 r = philox4x32_10(rc.v, rp.v, (key >> 2) & 31, (rc.epoch << 4) | kStreamAnchor, a.key0, a.key1);
+        slot = (uint32_t)pick32(r.x0, rc.deg);
+        cls = key & 3;
+    }
+}
+
+// The cached anchor of the walker's state, or need = true (no valid entry).
+__device__ __forceinline__ void anchor_lookup(const WalkArgs& a, const Row& rc, const Row& rp, int64_t ein,
+                                              uint64_t anc, uint32_t& an, uint32_t& cls, bool& need)
+{
+    need = true;
     if (ein >= 0) {
         const uint32_t tag = (uint32_t)(anc >> 32) & 0x3FFFFFFFu;
         if (anc != kAnchorNone64 && tag >= rc.epoch) {
-            const uint32_t an = (uint32_t)anc;
+            need = false;
+            an = (uint32_t)anc;
             if (tag >= rp.epoch) {
                 cls = (uint32_t)(anc >> 62);
             } else {
                 cls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + an]);
                 a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
             }
-            return an;
         }
     }
-    const uint32_t an = anchor_init(a, rc, rp, cls);
-    if (ein >= 0) a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+}
+
+// Called by every active lane of the wave together (WEIGHT inits are wave-cooperative).
+__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, int64_t ein,
+                                               uint64_t anc, uint32_t& cls)
+{
+    uint32_t an = 0;
+    bool need;
+    anchor_lookup(a, rc, rp, ein, anc, an, cls, need);
+    if (a.init == kInitWeight) {
+        anchor_init_wave(a, need, rc, rp, an, cls);
+    } else if (need) {
+        an = anchor_init(a, rc, rp, cls);
+    }
+    if (need && ein >= 0) a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     return an;
 }
 

@@ -45,7 +45,7 @@ for s in "$@"; do
             step probe_mh_nochunk 300 env WHARF_NO_CHUNKED_SCAN=1 python tools/rewalk_probe.py --batches 3 ;;
     ab)     for v in cur ${AB:-$(ls tools/ab 2>/dev/null | sed -n 's/^lib_\(.*\)\.so$/\1/p')}; do
               lib=""; [ $v = cur ] || lib=tools/ab/lib_$v.so
-              step ab_det_$v 300 env WHARF_LIB_PATH=$lib python tools/rewalk_probe.py --det --batches 3
+              step ab_${ABTAG:-det}_$v 300 env WHARF_LIB_PATH=$lib python tools/rewalk_probe.py ${PROBE:---det --batches 3}
             done ;;
     n2vinit) for i in random burnin weight; do
               step n2v_init_$i 300 python tools/rewalk_probe.py --model node2vec --batches 3 --init $i
