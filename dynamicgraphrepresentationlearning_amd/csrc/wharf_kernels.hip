@@ -194,9 +194,6 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
 // proposal of maximal weight (strict '>', metropolis_hastings_sampler.h:84-93).
 // Proposals need no has_edge when q == 1 (triangle and outward weigh the
 // same) or when prev's neighbour filter says no (exact).
-#ifndef WHARF_COOP_FENCE
-#define WHARF_COOP_FENCE 0
-#endif
 #ifndef WHARF_INIT_ROUNDS
 #define WHARF_INIT_ROUNDS 2
 #endif
@@ -219,16 +216,9 @@ __device__ __forceinline__ uint32_t nth_set_lane(uint64_t mask, uint32_t t)   //
     return lo;
 }
 
-__device__ __forceinline__ void wave_lds_sync()
-{
-#if WHARF_COOP_FENCE
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
-    __builtin_amdgcn_wave_barrier();
-#endif
-}
+// LDS traffic of one wave is processed in order; the barrier keeps the
+// compiler from moving the per-init table accesses across the phases
+__device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_wave_barrier(); }
 
 __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, const Row& rp, uint32_t& slot,
                                  uint32_t& cls)
