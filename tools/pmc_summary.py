@@ -29,11 +29,13 @@ def per_launch(path, kernel, counter, skip=0):
     return vals[skip:]
 
 
-def trace_avg_ns(path, kernel, skip=0):
-    """average duration from a --kernel-trace csv, dispatch order, first `skip` launches dropped"""
+def trace_avg_ns(path, kernel, skip=0, take=0):
+    """average duration from a --kernel-trace csv, dispatch order, first `skip` launches dropped
+    (then the next `take`, if given: the bench's timed steps, not its later configs[2] launches)"""
     rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[skip:]]
+    rows = rows[skip:skip + take] if take else rows[skip:]
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
     return statistics.mean(d) if d else None
 
 
@@ -47,6 +49,8 @@ def main():
     ap.add_argument("--trace", default=None, help="rocprofv3 --kernel-trace kernel_trace.csv (with --skip)")
     ap.add_argument("--skip", type=int, default=0,
                     help="drop the first launches (node2vec: the first generation also initialises every anchor)")
+    ap.add_argument("--trace-skip", type=int, default=None, help="launches to drop in the trace (default: --skip)")
+    ap.add_argument("--trace-take", type=int, default=0, help="launches to keep in the trace after the skipped ones")
     ap.add_argument("--round", default="r01")
     ap.add_argument("--algorithmic-bytes", type=float, default=None)
     a = ap.parse_args()
@@ -54,7 +58,7 @@ def main():
     w = per_launch(a.write, a.kernel, "WRITE_SIZE", a.skip)
     avg_ns = None
     if a.trace:
-        avg_ns = trace_avg_ns(a.trace, a.kernel, a.skip)
+        avg_ns = trace_avg_ns(a.trace, a.kernel, a.skip if a.trace_skip is None else a.trace_skip, a.trace_take)
     else:
         for r in csv.DictReader(open(a.stats)):
             if a.kernel in r["Name"]:
