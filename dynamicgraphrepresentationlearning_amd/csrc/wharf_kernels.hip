@@ -191,7 +191,7 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
 // the call, whichever they are (that version: configs[2] node2vec
 // re-walk batch 84 ms, first generation 224 ms).  A per-init LDS minimum over
 // (weight rank, proposal index) keeps the reference's choice: the first
-// proposal of maximal weight (strict '>', metropolis_hastings_sampler.h:84-93).
+// proposal of maximal weight (strict '>', metropolis_hastings_sampler.h:87-107).
 // Proposals need no has_edge when q == 1 (triangle and outward weigh the
 // same) or when prev's neighbour filter says no (exact).
 #ifndef WHARF_INIT_ROUNDS
@@ -422,6 +422,10 @@ __device__ __forceinline__ void walk_state(const WalkArgs& a, uint32_t cur, uint
             uint64_t unused;
             w.rp = load_edge<MODEL, DET>(a, w.rc.off + pick32(q.x0, w.rc.deg), unused);
         }
+        // (At a re-walk start cur is a batch source reset in this epoch, so the
+        // entry found here is one another walker initialised in this epoch;
+        // skipping the search and initialising instead gives the same corpus but
+        // many more inits: configs[2] node2vec re-walk 73 -> 93 ms.)
         if (w.rc.deg) {
             w.ein = row_find(a.adj, w.rp, w.rc.v);
             if (w.ein >= 0) w.anc = a.anchor[(uint64_t)w.ein * kAnchorStride];
