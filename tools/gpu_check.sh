@@ -57,6 +57,7 @@ for s in "$@"; do
     c5n2vq) step c5_node2vec_q 1100 python tools/bigscale.py --model node2vec --wpv 1 --batches 4 --mixed --no-oracle ;;
     n2v)    step bench_n2v 900 python bench.py --model node2vec --steps 2 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     dist2)  step bench_dist2 900 env WHARF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --scale 20 --samples 29296270 --stream-samples 10000000 --steps 3 --warmup 1 --rewalk-batches 5 ;;
+    dist4)  step bench_dist4 900 env WHARF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 4 --scale 20 --samples 29296270 --stream-samples 10000000 --steps 3 --warmup 1 --rewalk-batches 5 --det-rewalk-batches 3 ;;
     dist2full) step bench_dist2_full 900 env WHARF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --rewalk-batches 5 ;;
     prof)   step prof_gen 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_gen -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-baseline off ;;
     pmc)    step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 0 --rewalk-batches 0 --cpu-baseline off
