@@ -8,6 +8,8 @@
 //   dep    next slot depends on the loaded record (pointer chasing, like a walk)
 //   indep  slots from a counter hash (no dependency: max memory-level parallelism)
 //   stream the same bytes read sequentially (HBM streaming ceiling)
+//   dep_64B_block / dep_128B_block: each gather reads the whole aligned 64-B /
+//   128-B block around its slot (calibrates what one 16-B gather fetches)
 //
 // Second argument: table memory kind — "coarse" (hipMalloc, default),
 // "uncached" (hipDeviceMallocUncached: requests bypass L2 line fills) or
@@ -76,6 +78,11 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ t, uin
             const uint2* t2 = reinterpret_cast<const uint2*>(t);
             const uint2 q = t2[__umulhi(x, (uint32_t)n) * 2 + (x & 1)];
             r = make_uint4(q.x, q.y, 0, 0);
+        } else if (MODE == 13 || MODE == 14) {   // dep, a whole 64-B / 128-B aligned block per gather
+            const int k = MODE == 13 ? 4 : 8;
+            const uint4* b = t + (slot & ~(uint64_t)(k - 1));
+            r = b[0];
+            for (int j = 1; j < k; j++) { const uint4 q = b[j]; r.x ^= q.x; r.y ^= q.y; }
         } else if (MODE == 3) {
             typedef unsigned int v4u __attribute__((ext_vector_type(4)));
             const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(t + slot));
@@ -136,11 +143,11 @@ int main(int argc, char** argv)
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
-    const char* names[13] = {"dep", "indep", "stream", "dep_nt", "dep_philox", "dep_4B", "dep_8B", "dep_nostore",
+    const char* names[15] = {"dep", "indep", "stream", "dep_nt", "dep_philox", "dep_4B", "dep_8B", "dep_nostore",
                              "dep_store16B_per_4", "dep_store_same_row", "dep_store_nt",
-                             "dep_store_lds16_tiled", "dep_store_lds16_rows"};
+                             "dep_store_lds16_tiled", "dep_store_lds16_rows", "dep_64B_block", "dep_128B_block"};
     for (int rep = 0; rep < 2; rep++)
-        for (int mode = 0; mode < 13; mode++) {
+        for (int mode = 0; mode < 15; mode++) {
             if (only && std::strcmp(only, names[mode]) != 0) continue;
             CHK(hipEventRecord(a));
             if (mode == 0) hipLaunchKernelGGL(k_gather<0>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
@@ -156,6 +163,8 @@ int main(int argc, char** argv)
             if (mode == 10) hipLaunchKernelGGL(k_gather<10>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 11) hipLaunchKernelGGL(k_gather<11>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 12) hipLaunchKernelGGL(k_gather<12>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 13) hipLaunchKernelGGL(k_gather<13>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 14) hipLaunchKernelGGL(k_gather<14>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             CHK(hipEventRecord(b));
             CHK(hipEventSynchronize(b));
             float ms;

@@ -34,6 +34,11 @@ for s in "$@"; do
                step ls_c5_$t 600 env WHARF_LOCKSTEP_MIN=$t python tools/bigscale.py --model node2vec --wpv 1 --batches 2 --mixed
              done ;;
     roof)   step gather_roof 300 tools/gather_roof 3.48 ;;
+    roofcal) for m in dep dep_64B_block dep_128B_block; do
+              step roofcal_$m 120 tools/gather_roof 3.48 coarse $m
+              step roofcal_fetch_$m 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/roofcal_fetch_$m -o run -- tools/gather_roof 3.48 coarse $m
+              step roofcal_req_$m 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d gpurun_out/roofcal_req_$m -o run -- tools/gather_roof 3.48 coarse $m
+            done ;;
     big)    step bigscale 900 python tools/bigscale.py ;;
     index)  step index_probe 800 python tools/index_probe.py ;;
     c4)     step c4_stream 1100 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 50 ;;
