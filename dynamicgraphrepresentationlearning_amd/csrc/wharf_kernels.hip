@@ -182,22 +182,22 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
 // state it enters: `anc` is that entry, carried by the walker.
 //
 // WEIGHT inits are evaluated by the whole wave at once (anchor_init_wave):
-// the lanes that need one publish their (cur, prev) rows, and the wave's 64
-// lanes evaluate the 21 proposals of every such init side by side — targets,
-// then prev's filter words, then has_edge for filter positives, each one
-// round of independent loads for up to kInitRounds proposals per active lane — instead
-// of each lane walking its 21 proposals in dependent groups of 4 while the
-// rest of its (lock-step) wave waits; proposals go to the lanes active at
-// the call, whichever they are (that version: configs[2] node2vec
-// re-walk batch 84 ms, first generation 224 ms).  A per-init LDS minimum over
-// (weight rank, proposal index) keeps the reference's choice: the first
-// proposal of maximal weight (strict '>', metropolis_hastings_sampler.h:87-107).
-// Proposals need no has_edge when q == 1 (triangle and outward weigh the
-// same) or when prev's neighbour filter says no (exact).
+// the lanes that need one publish their (cur, prev) rows, and the proposals
+// of all of them (21 each) are dealt over the lanes active at the call,
+// whichever they are.  Targets, then prev's filter words, then has_edge for
+// filter positives: each one round of independent loads for up to
+// kInitRounds proposals per active lane.  Before, each lane walked its 21
+// proposals in dependent groups of 4 while the rest of its lock-step wave
+// waited (configs[2] node2vec re-walk 88.6 ms, first generation 224 ms; now
+// 76.7 / 178 ms).  A per-init LDS minimum over (weight rank, proposal index)
+// keeps the reference's choice: the first proposal of maximal weight (strict
+// '>', metropolis_hastings_sampler.h:87-107).  Proposals need no has_edge
+// when q == 1 (triangle and outward weigh the same) or when prev's neighbour
+// filter says no (exact).
 #ifndef WHARF_INIT_ROUNDS
 #define WHARF_INIT_ROUNDS 2
 #endif
-constexpr uint32_t kInitRounds = WHARF_INIT_ROUNDS;   // 64-proposal rounds in flight
+constexpr uint32_t kInitRounds = WHARF_INIT_ROUNDS;   // proposals per active lane in flight
 constexpr uint32_t kWavesPerBlock = 4;                // every walk kernel runs 256-thread blocks
 
 struct InitReq {     // a lane's init, published for the wave
