@@ -227,6 +227,7 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
     __shared__ uint32_t s_key[kWavesPerBlock][64];
     const uint64_t mask = __ballot(need);
     if (!mask) return;
+    if (blockDim.x > 64 * kWavesPerBlock) __builtin_trap();   // the per-wave LDS tables assume <= 4 waves
     // proposals are dealt over the lanes active here (the caller's walking lanes), not all 64
     const uint64_t act = __ballot(1), below = (1ull << __lane_id()) - 1;
     const uint32_t wv = threadIdx.x >> 6, nact = (uint32_t)__popcll(act), lane = (uint32_t)__popcll(act & below);
