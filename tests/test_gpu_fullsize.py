@@ -14,7 +14,10 @@ bit for bit and the rest is checked structurally:
   the number of re-walked transitions;
 
   the same batch in deterministic mode: every re-walked suffix equals the walk
-  of its round from its batch source on the new graph.
+  of its round from its batch source on the new graph;
+
+  configs[1] generation with node2vec MH (every anchor initialised, wave-
+  cooperatively): step count, transitions, a 4096-walk window vs the oracle.
 """
 import numpy as np
 import pytest
@@ -164,3 +167,30 @@ def test_configs2_full_size_deterministic_batch(W, torch):
         assert torch.equal(after[pos][m], exp), f"re-walked suffix differs from the walk from its source at {pos}"
         walked += int((after[pos][m] != sent).sum())
     assert walked == steps
+
+
+def test_configs1_full_size_node2vec_generation(W, torch):
+    """node2vec MH (p = .5, q = 2, WEIGHT inits) on the configs[1] graph: every
+    anchor is new, so ~10^8 wave-cooperative inits run; the step count is
+    exact, sampled transitions are edges, and a 4096-walk window is identical
+    to the oracle's (which computes every anchor it needs on its own)."""
+    n = 1 << 22
+    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=L, model=W.NODE2VEC, paramP=0.5, paramQ=2.0,
+                        deterministic=False, seed=0x5EED)
+    g = W.WharfMH.from_rmat(n, 117_185_083, 2 * n, seed=2, config=cfg)
+    off, adj = g.flatten_graph()
+    ekeys, deg = _edge_keys(torch, off, adj, n)
+    g.generate_initial_random_walks()
+    st = g.stats()
+    assert st["steps"] == int((deg > 0).sum()) * 10 * (L - 1) and 0 < st["accepts"] < st["steps"]
+    w = _dev_walks(torch, g)
+    wid = torch.arange(w.shape[1], device="cuda:0")
+    live = deg[wid % n] > 0
+    for p in (0, 1, 40, 78):
+        assert _all_edges(torch, ekeys, n, w[p, live], w[p + 1, live]), f"non-edge transition at {p}"
+    w0 = 17_000_000
+    ref = O.Engine(off, adj, wpv=10, L=L, model=O.NODE2VEC, p=0.5, q=2.0, deterministic=False, seed=0x5EED)
+    ref.time_generate_range(w0, w0 + 4096)
+    mine = w[:, w0:w0 + 4096].T.contiguous().cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(mine, ref.walks_range(w0, w0 + 4096))
+    g.destroy()
