@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--batches", type=int, default=1)
     ap.add_argument("--mixed", action="store_true", help="insert batch b, then delete it")
     ap.add_argument("--no-oracle", action="store_true")
+    ap.add_argument("--det", action="store_true", help="deterministic mode (DeepWalk)")
     a = ap.parse_args()
     import torch
     import dynamicgraphrepresentationlearning_amd as W
@@ -45,7 +46,7 @@ def main():
 
     n = 1 << a.scale
     node2vec = a.model == "node2vec"
-    cfg = W.WharfConfig(walks_per_vertex=a.wpv, walk_length=80, deterministic=False, seed=11,
+    cfg = W.WharfConfig(walks_per_vertex=a.wpv, walk_length=80, deterministic=a.det, seed=11,
                         model=W.NODE2VEC if node2vec else W.DEEPWALK, paramP=0.5, paramQ=2.0)
     t0 = time.time()
     # seed 4: odd RMAT multiplier, no sample-period repeats below 2^31 samples
@@ -82,7 +83,7 @@ def main():
     same = None
     if not node2vec and not a.no_oracle:
         w0 = int(n // 3)
-        ref = O.Engine(off, adj, wpv=a.wpv, L=80, deterministic=False, seed=11)
+        ref = O.Engine(off, adj, wpv=a.wpv, L=80, deterministic=a.det, seed=11)
         ref.time_generate_range(w0, w0 + 2048)
         mine = np.stack([np.pad(g.walk_vertices(w), (0, 80 - len(g.walk_vertices(w))), constant_values=W.SENTINEL)
                          for w in range(w0, w0 + 2048)])
@@ -114,7 +115,7 @@ def main():
     last = W.generate_batch_of_edges(5000, n, a.batches - 1, False, False)
     g.delete_edges_batch(last, remove_dups=True, out=out)
     m3 = g.number_of_edges()
-    res = {"config": f"RMAT scale {a.scale}, {a.samples} undirected samples (seed 4), {a.model} MH, wpv {a.wpv}, "
+    res = {"config": f"RMAT scale {a.scale}, {a.samples} undirected samples (seed 4), {a.model} {'deterministic' if a.det else 'MH'}, wpv {a.wpv}, "
                      f"L 80, {a.batches} {'insert+delete' if a.mixed else 'insert'} batches of "
                      "generate_batch_of_edges(5000, n, b, false, false)",
            "n": n, "m": m, "walks": g.number_of_walks, "build_s": round(t_build, 1),

@@ -42,6 +42,7 @@ for s in "$@"; do
     big)    step bigscale 900 python tools/bigscale.py ;;
     index)  step index_probe 800 python tools/index_probe.py ;;
     c4)     step c4_stream 1100 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 50 ;;
+    c4det)  step c4_det 1100 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 10 --det ;;
     c5n2v)  step c5_node2vec 1100 python tools/bigscale.py --model node2vec --wpv 1 --batches 10 --mixed ;;
     detnm)  step bench_det_nomemo 900 env WHARF_NO_MEMO=1 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     chunk)  step probe_det 300 python tools/rewalk_probe.py --det --batches 3
