@@ -57,6 +57,10 @@ for s in "$@"; do
               step n2v_init_$i 300 python tools/rewalk_probe.py --model node2vec --batches 3 --init $i
             done
             step n2v_q1 300 python tools/rewalk_probe.py --model node2vec --batches 3 --p 4 --q 1 ;;
+    abn2v)  for v in cur ${AB:-}; do
+              lib=""; [ $v = cur ] || lib=tools/ab/lib_$v.so
+              step abn2v_$v 600 env WHARF_LIB_PATH=$lib python bench.py --model node2vec --steps 2 --warmup 1 --rewalk-batches 3 --det-rewalk-batches 0 --cpu-baseline off
+            done ;;
     det)    step bench_det 900 python bench.py --det --steps 3 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     n2vnf)  step bench_n2v_nofilter 900 env WHARF_NO_NEIGHBOUR_FILTER=1 python bench.py --model node2vec --steps 2 --warmup 1 --rewalk-batches 5 --cpu-baseline off ;;
     c5n2vnf) step c5_node2vec_nofilter 1100 env WHARF_NO_NEIGHBOUR_FILTER=1 python tools/bigscale.py --model node2vec --wpv 1 --batches 4 --mixed --no-oracle ;;
