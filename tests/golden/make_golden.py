@@ -8,6 +8,7 @@ the GPU box); the committed outputs are data: inputs and the reference's
 outputs for them.
 
     python tests/golden/make_golden.py            # writes tests/golden/*
+    python tests/golden/make_golden.py mh-matrix  # only the MH statistics matrix (merged into golden.json)
 """
 from __future__ import annotations
 
@@ -104,6 +105,69 @@ def mh_class_fractions(walks, off, adj):
                 out += 1
     t = ret + tri + out
     return {"return": ret / t, "triangle": tri / t, "outward": out / t, "transitions": t}
+
+
+MH_SEEDS = tuple(range(1, 9))
+MH_INITS = ("random", "burnin", "weight")
+MH_PQ = ((0.5, 2.0), (4.0, 1.0), (2.0, 0.5))
+
+
+def _mh_cell(args):
+    """One reference MH run (serial, config::random.reinit(seed)) on wiki: the
+    transition-class fractions of its corpus."""
+    tmp, csr, model, p, q, init, seed = args
+    d = os.path.join(tmp, f"mhm_{model}_{p}_{q}_{init}_{seed}")
+    os.makedirs(d, exist_ok=True)
+    run(["out", d, "cfg", 10, 80, model, p, q, init, 0, seed, "graph-csr", csr, "gen"])
+    wm = read_walks(d, "0_gen", 80)
+    shutil.rmtree(d, ignore_errors=True)
+    return wm
+
+
+def mh_matrix(tmp, woff, wadj):
+    """Reference MH-mode statistics over seeds x sampler init x (p, q) on wiki
+    (metropolis_hastings_sampler.h:69-122, node2vec.h:74-119): per cell the
+    mean and sample sd over the seeds of the return / triangle / outward
+    fractions, so a test can derive its tolerance from the reference's own
+    seed-to-seed spread.  DeepWalk: the same fractions (uniform walk)."""
+    from concurrent.futures import ThreadPoolExecutor
+    csr = os.path.join(tmp, "wiki_mh.csr")
+    write_csr(csr, woff, wadj)
+    jobs = [(tmp, csr, "node2vec", p, q, init, s) for (p, q) in MH_PQ for init in MH_INITS for s in MH_SEEDS]
+    jobs += [(tmp, csr, "deepwalk", 1.0, 1.0, "weight", s) for s in MH_SEEDS]
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        walks = list(ex.map(_mh_cell, jobs))
+    cells = {}
+    for j, wm in zip(jobs, walks):
+        _, _, model, p, q, init, s = j
+        key = f"{model}_p{p}_q{q}_{init}" if model == "node2vec" else "deepwalk"
+        cells.setdefault(key, []).append(mh_class_fractions(wm, woff, wadj))
+    out = {"seeds": list(MH_SEEDS), "graph": "wiki (tests/golden/wiki_csr.npz)", "wpv": 10, "L": 80,
+           "generator": "ref_harness cfg 10 80 <model> <p> <q> <init> 0 <seed> graph-csr wiki gen, NUM_THREADS=1"}
+    for key, fr in cells.items():
+        c = {"transitions": fr[0]["transitions"]}
+        for k in ("return", "triangle", "outward"):
+            v = np.array([f[k] for f in fr])
+            c[k] = {"mean": float(v.mean()), "sd": float(v.std(ddof=1)), "per_seed": [float(x) for x in v]}
+        out[key] = c
+    return out
+
+
+def main_mh_matrix():
+    if not os.path.exists(HARNESS):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
+    z = np.load(os.path.join(HERE, "wiki_csr.npz"))
+    tmp = tempfile.mkdtemp(prefix="golden_mh_")
+    try:
+        mm = mh_matrix(tmp, z["off"], z["adj"])
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    path = os.path.join(HERE, "golden.json")
+    meta = json.load(open(path))
+    meta["mh_matrix_reference"] = mm
+    with open(path, "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("mh_matrix_reference written to", path)
 
 
 def main():
@@ -247,6 +311,7 @@ def main():
                 st["dof"] = dof
             mh[f"{model}_p{p}_q{q}"] = st
         meta["mh_stats_reference"] = mh
+        meta["mh_matrix_reference"] = mh_matrix(tmp, woff, wadj)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     with open(os.path.join(HERE, "golden.json"), "w") as f:
@@ -255,4 +320,4 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(main_mh_matrix() if sys.argv[1:] == ["mh-matrix"] else main())

@@ -1,0 +1,77 @@
+"""Shared helpers for the MH-mode statistical link to the reference.
+
+The reference's MH mode draws from one global RNG (`config::random`,
+`config/globals.h:26`), so its corpus is reproducible only serially and only for
+its own RNG; our Philox streams give different walks.  What must agree is the
+*distribution*: per (model, p, q, sampler init) cell, the fractions of node2vec
+transition classes — return (next == prev), triangle (edge prev-next) and
+outward — that the frozen-anchor MH sampler produces
+(`walks/metropolis_hastings_sampler.h:69-122`, `walks/models/node2vec.h:74-119`).
+
+`tests/golden/make_golden.py mh-matrix` ran the reference over seeds 1..8 per
+cell on wiki-graph and committed the mean and sample sd per fraction
+(`golden.json` `mh_matrix_reference`).  A build run over the same number of
+seeds passes a cell when each fraction's mean lies within
+`Z_TOL` standard errors of the reference mean, the standard error of the
+difference being sqrt(sd_ref^2/k_ref + sd_ours^2/k_ours) — the tolerance comes
+from the reference's own seed-to-seed spread, not from a hand-picked band.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SENT = 0xFFFFFFFE
+Z_TOL = 4.0
+CLASSES = ("return", "triangle", "outward")
+SD_FLOOR = 5e-5     # guards cells whose 8 seeds happen to agree to 4 digits
+
+
+def cells(matrix: dict):
+    """(key, model, p, q, init name) of every cell in mh_matrix_reference."""
+    out = []
+    for key, c in sorted(matrix.items()):
+        if not isinstance(c, dict) or "return" not in c:
+            continue
+        if key == "deepwalk":
+            out.append((key, "deepwalk", 1.0, 1.0, "weight"))
+        else:
+            _, ps, qs, init = key.split("_")
+            out.append((key, "node2vec", float(ps[1:]), float(qs[1:]), init))
+    return out
+
+
+def class_fractions(walks: np.ndarray, off: np.ndarray, adj: np.ndarray) -> np.ndarray:
+    """[return, triangle, outward] over every transition walk[pos] -> walk[pos+1],
+    pos >= 1, classified against walk[pos-1] (the same count as make_golden.py's
+    mh_class_fractions)."""
+    a = walks[:, :-2].ravel().astype(np.int64)
+    c = walks[:, 2:].ravel().astype(np.int64)
+    k = c != SENT
+    a, c = a[k], c[k]
+    ret = a == c
+    n = len(off) - 1
+    src = np.repeat(np.arange(n, dtype=np.int64), np.diff(off.astype(np.int64)))
+    ekeys = src * n + adj.astype(np.int64)
+    q = a * n + c
+    j = np.minimum(np.searchsorted(ekeys, q), max(len(ekeys) - 1, 0))
+    tri = (ekeys[j] == q) & ~ret
+    t = len(a)
+    r, e = ret.sum() / t, tri.sum() / t
+    return np.array([r, e, 1.0 - r - e])
+
+
+def check_cell(ref_cell: dict, ours: np.ndarray, label: str) -> list[str]:
+    """ours: [k_seeds, 3] fractions.  Returns the failures (empty = pass)."""
+    k = ours.shape[0]
+    mu = ours.mean(0)
+    sd = ours.std(0, ddof=1) if k > 1 else np.zeros(3)
+    bad = []
+    for i, cl in enumerate(CLASSES):
+        rm = ref_cell[cl]["mean"]
+        rs = max(ref_cell[cl]["sd"], SD_FLOOR)
+        kr = len(ref_cell[cl]["per_seed"])
+        se = np.sqrt(rs ** 2 / kr + max(sd[i], SD_FLOOR) ** 2 / k)
+        z = (mu[i] - rm) / se
+        if abs(z) > Z_TOL:
+            bad.append(f"{label} {cl}: ours {mu[i]:.5f} ref {rm:.5f} (sd {rs:.5f}) z={z:.1f}")
+    return bad

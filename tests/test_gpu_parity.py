@@ -13,6 +13,7 @@ import os
 import numpy as np
 import pytest
 
+import mh_stats
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -400,32 +401,39 @@ def test_mh_deepwalk_bit_exact_and_uniform(W):
     del pos
 
 
-def test_mh_node2vec_statistics_vs_reference(W, meta):
-    """Transition classes on wiki-graph, node2vec p=0.5 q=2, WEIGHT init:
-    the reference (frozen-anchor MH, serial) returns to prev 54.3 % of the time."""
+_MATRIX = json.load(open(os.path.join(G, "golden.json")))["mh_matrix_reference"]
+
+
+@pytest.mark.parametrize("cell", mh_stats.cells(_MATRIX), ids=lambda c: c[0])
+def test_mh_matrix_vs_reference(W, cell):
+    """Every (model, p, q, sampler init) cell of the reference's MH statistics
+    (8 reference seeds per cell, `make_golden.py mh-matrix`): the HIP path over
+    the same 8 seeds gives return / triangle / outward fractions within
+    mh_stats.Z_TOL standard errors of the reference means, the standard error
+    coming from the reference's own seed-to-seed sd
+    (metropolis_hastings_sampler.h:69-122, node2vec.h:74-119)."""
+    key, model, p, q, init = cell
     z = np.load(os.path.join(G, "wiki_csr.npz"))
     off, adj = z["off"], z["adj"]
-    refst = meta["mh_stats_reference"]["node2vec_p0.5_q2.0"]
-    fr = []
-    for seed in (1, 2, 3):
-        cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, model=W.NODE2VEC, paramP=0.5, paramQ=2.0,
-                            deterministic=False, seed=seed)
+    inits = {"random": 0, "burnin": 1, "weight": 2}
+    ours = []
+    for s in _MATRIX["seeds"]:
+        cfg = W.WharfConfig(walks_per_vertex=_MATRIX["wpv"], walk_length=_MATRIX["L"],
+                            model=W.NODE2VEC if model == "node2vec" else W.DEEPWALK, paramP=p, paramQ=q,
+                            sampler_init=inits[init], deterministic=False, seed=s)
         g = W.WharfMH.from_csr(off, adj, config=cfg)
         g.generate_initial_random_walks()
         w = g.walks()
-        a, b, c = w[:, :-2].ravel(), w[:, 1:-1].ravel(), w[:, 2:].ravel()
-        k = c != W.SENTINEL
-        a, c = a[k].astype(np.int64), c[k].astype(np.int64)
-        ret = (a == c)
-        edge = _has_edge(off, adj, a, c) & ~ret
-        t = len(a)
-        fr.append((ret.sum() / t, edge.sum() / t))
+        if s == _MATRIX["seeds"][0]:      # and the corpus is the oracle's, bit for bit
+            ref = O.Engine(off, adj, wpv=_MATRIX["wpv"], L=_MATRIX["L"], model=cfg.model, p=p, q=q,
+                           init=inits[init], deterministic=False, seed=s)
+            ref.generate()
+            np.testing.assert_array_equal(w, ref.walks())
+            assert g.stats()["accepts"] == ref.accepts
+        ours.append(mh_stats.class_fractions(w, off, adj))
         g.destroy()
-    r = np.mean([f[0] for f in fr])
-    tri = np.mean([f[1] for f in fr])
-    # the anchor draw per (cur, prev) state dominates the variance: +-0.02 absolute
-    assert abs(r - refst["return"]) < 0.02, (r, refst)
-    assert abs(tri - refst["triangle"]) < 0.02, (tri, refst)
+    bad = mh_stats.check_cell(_MATRIX[key], np.array(ours), key)
+    assert not bad, bad
 
 
 # ---------------------------------------------------------------------------
