@@ -474,6 +474,9 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         // 4. new CSR: offsets, moved old edges, placed new edges; samplers of
         //    the batch sources are reset (wharfmh.h:504-540, 652-690)
         const uint64_t m_new = insert ? h->m + total_chg : h->m - total_chg;
+        // row epochs live in 24 bits of the records (wharf_device.h make_rec) and
+        // feed the Philox counters: refuse the batch that would wrap them
+        REQUIRE(h->epoch + 1 < (1u << kEpochBits), WHARF_E_INVALID, "update epoch limit (2^24 applied batches) reached");
         h->epoch++;
         h->runs.ensure(k * sizeof(RunInfo));
         HIPCHK(hipMemsetAsync(h->bitmap.p, 0, (h->bitmap_words() + kBloomWords) * 4, s));

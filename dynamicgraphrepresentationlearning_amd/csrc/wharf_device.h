@@ -40,6 +40,7 @@ struct Row {          // unpacked, in registers
 };
 constexpr uint64_t kOffBits = 40;
 constexpr uint64_t kOffMask = (1ull << kOffBits) - 1;
+constexpr uint32_t kEpochBits = 64 - kOffBits;   // row epoch: the record's top 24 bits
 constexpr uint64_t kAnchorNone64 = ~0ull;
 constexpr uint64_t kAnchorStride = 4;         // u64 words between anchor entries (32-B node2vec edge records)
 constexpr uint64_t kEmptyKey = ~0ull;         // empty slot of the edge hash set

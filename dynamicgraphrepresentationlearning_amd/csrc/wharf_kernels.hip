@@ -167,15 +167,20 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
 // its global CSR slot, or -1), tagged with the epoch it was written in.  The
 // reference keeps the sampler in cur's SamplerManager (wharfmh.h:296-301),
 // which is reset only when cur is a batch source (wharfmh.h:504,539): the
-// anchor stays valid while cur's row is unchanged since the tag.  Every
-// writer of an entry writes the same value, a pure function of the current
-// snapshot, so lazy races are benign and the result does not depend on which
-// walks (or which GPU) touched it first.
-// The entry also keeps the anchor's weight class, so an accepted step needs
-// one has_edge, not two.  The class depends on prev's row (node2vec.h:74-88
-// evaluates has_edge(prev, anchor) on the current graph at every sample()):
-// when prev was a batch source since the tag, the anchor stands and only its
-// class is re-evaluated and re-tagged.  Entry = slot | tag << 32 | class << 62.
+// anchor stays valid while cur's row is unchanged since the tag (checked here)
+// AND while prev's row is unchanged — the entry sits in prev's row, which a
+// batch rebuilds with empty entries (k_move_edges, k_erec_rows).  That second
+// reset is a deliberate divergence: the reference's surviving
+// sampler was initialised against prev's row as it was at the first visit, a
+// function of which walks visited the state when, which differs per GPU shard;
+// re-initialising keeps every entry a pure function of the current snapshot
+// (same Philox proposals, since cur's row epoch is unchanged; only the weight
+// classes prev's new row gives them can change the pick), so lazy races are
+// benign and the corpus does not depend on which walks (or which GPU) touched
+// it first.  The entry also keeps the anchor's weight class (node2vec.h:74-88,
+// has_edge(prev, anchor)), valid with the entry since prev's row is unchanged,
+// so an accepted step needs one has_edge, not two.
+// Entry = slot | tag << 32 | class << 62.
 //
 // node2vec MH keeps the entry of slot e inside e's 32-B edge record (bytes
 // 16-23), so the gather that crosses an edge also brings the anchor of the
@@ -204,17 +209,6 @@ struct InitReq {     // a lane's init, published for the wave
     uint32_t cv, cdeg, cep, pv, pdeg;
     uint64_t coff, poff, fd;
 };
-
-__device__ __forceinline__ uint32_t nth_set_lane(uint64_t mask, uint32_t t)   // lane of the t-th set bit
-{
-    uint32_t lo = 0;
-#pragma unroll
-    for (uint32_t w = 32; w > 0; w >>= 1) {
-        const uint32_t below = (uint32_t)__popcll(mask & ((1ull << (lo + w)) - 1));
-        if (below <= t) lo += w;
-    }
-    return lo;
-}
 
 // LDS traffic of one wave is processed in order; the barrier keeps the
 // compiler from moving the per-init table accesses across the phases
@@ -297,12 +291,7 @@ __device__ __forceinline__ void anchor_lookup(const WalkArgs& a, const Row& rc, 
         if (anc != kAnchorNone64 && tag >= rc.epoch) {
             need = false;
             an = (uint32_t)anc;
-            if (tag >= rp.epoch) {
-                cls = (uint32_t)(anc >> 62);
-            } else {
-                cls = weight_class<kNode2Vec>(a, rp, a.adj[rc.off + an]);
-                a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
-            }
+            cls = (uint32_t)(anc >> 62);
         }
     }
 }
@@ -1644,7 +1633,8 @@ void launch_move_records_inplace(ERec* rec, uint32_t rs, uint64_t m, uint64_t S,
 }
 
 // records of the rebuilt source rows: erec[slot] = vrec[adj[slot]] (block per
-// run); their anchor entries are reset (the source's samplers are)
+// run); their anchor entries (states (target, source), whose anchors read the
+// source's row) start empty: see anchor_lookup and DESIGN.md §4
 __global__ void k_erec_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ noff,
                             const uint32_t* __restrict__ nadj, const ERec* __restrict__ vrec, ERec* __restrict__ erec,
                             uint32_t rs)

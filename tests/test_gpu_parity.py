@@ -349,6 +349,28 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     _compare_stream(W, off, adj, batches, wpv=3, L=40, **kw)
 
 
+@pytest.mark.parametrize("force", ["0", "1", "2"])   # record patch / in place / gather rebuild
+@pytest.mark.parametrize("init", [1, 2])             # BURNIN, WEIGHT: inits that read prev's row
+def test_node2vec_anchor_reset_with_prev_row(W, monkeypatch, force, init):
+    """The anchor of state (cur=c, prev=s) is cached in slot s->c of s's row.
+    Directed batches make s a source while its targets are not: s's rebuilt
+    row starts with empty entries, so (c, s) is re-initialised against s's new
+    row with the same Philox proposals (c's row epoch is unchanged) — the
+    shard-invariant rule of DESIGN.md §4 (the reference keeps c's sampler,
+    initialised against s's row at the first visit).  Exercised on all three
+    record paths, bit-exact against the oracle, which restates the same rule."""
+    monkeypatch.setenv("WHARF_FORCE_RECORD_REBUILD", force)
+    base = O.generate_batch_of_edges(30000, 1 << 12, 21, False, False)
+    off, adj = O.csr_from_edges(1 << 11, base)
+    R, A = O.REMOVE_DUPS, O.APPLY_WALK_UPDATES
+    batches = [(True, O.generate_batch_of_edges(400, 1 << 11, 31, False, True), R | A),
+               (False, O.generate_batch_of_edges(400, 1 << 11, 31, False, True), R | A),
+               (True, O.generate_batch_of_edges(300, 1 << 11, 32, False, True), R | A),
+               (False, O.generate_batch_of_edges(900, 1 << 11, 33, False, False), R | A)]
+    _compare_stream(W, off, adj, batches, wpv=4, L=30, model=1, paramP=0.5, paramQ=2.0, sampler_init=init,
+                    deterministic=False, seed=4321)
+
+
 # ---------------------------------------------------------------------------
 # MH mode
 # ---------------------------------------------------------------------------
