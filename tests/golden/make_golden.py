@@ -153,6 +153,52 @@ def mh_matrix(tmp, woff, wadj):
     return out
 
 
+MH_STREAM_BATCHES = ((5000, 0), (3000, 100))   # (edges, seed offset): insert, then delete
+
+
+def _mh_stream_cell(args):
+    """Reference MH run through an insert and a delete batch (wharfmh.h:439-923
+    in MH mode: re-walks draw from config::random): the final corpus and graph."""
+    tmp, csr, p, q, init, seed = args
+    d = os.path.join(tmp, f"mhs_{p}_{q}_{init}_{seed}")
+    os.makedirs(d, exist_ok=True)
+    (mi, oi), (md, od) = MH_STREAM_BATCHES
+    run(["out", d, "cfg", 10, 80, "node2vec", p, q, init, 0, seed, "graph-csr", csr, "gen",
+         "ins", mi, seed + oi, 0, "del", md, seed + od, 0, "dump-graph"])
+    wm = read_walks(d, "2_del", 80)
+    off, adj = read_graph(d, "2")
+    shutil.rmtree(d, ignore_errors=True)
+    return mh_class_fractions(wm, off, adj)
+
+
+def mh_stream_matrix(tmp, woff, wadj):
+    """MH statistics of the corpus after an insert + delete batch on wiki
+    (undirected RMAT batches generate_batch_of_edges(M, n, seed + offset)),
+    classified against the final graph: pins the re-walk path and the sampler
+    resets of batch sources (wharfmh.h:504,539,652,689) statistically."""
+    from concurrent.futures import ThreadPoolExecutor
+    csr = os.path.join(tmp, "wiki_mhs.csr")
+    write_csr(csr, woff, wadj)
+    jobs = [(tmp, csr, 0.5, 2.0, init, s) for init in MH_INITS for s in MH_SEEDS]
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        res = list(ex.map(_mh_stream_cell, jobs))
+    out = {"seeds": list(MH_SEEDS), "graph": "wiki (tests/golden/wiki_csr.npz)", "wpv": 10, "L": 80,
+           "batches": [{"insert": True, "edges": MH_STREAM_BATCHES[0][0], "seed_offset": MH_STREAM_BATCHES[0][1]},
+                       {"insert": False, "edges": MH_STREAM_BATCHES[1][0], "seed_offset": MH_STREAM_BATCHES[1][1]}],
+           "generator": "ref_harness cfg 10 80 node2vec 0.5 2 <init> 0 <seed> graph-csr wiki gen "
+                        "ins 5000 <seed> 0 del 3000 <seed+100> 0, NUM_THREADS=1 (remove_dups=true)"}
+    cells = {}
+    for j, fr in zip(jobs, res):
+        cells.setdefault(f"node2vec_p{j[2]}_q{j[3]}_{j[4]}", []).append(fr)
+    for key, fr in cells.items():
+        c = {"transitions": [f["transitions"] for f in fr]}
+        for k in ("return", "triangle", "outward"):
+            v = np.array([f[k] for f in fr])
+            c[k] = {"mean": float(v.mean()), "sd": float(v.std(ddof=1)), "per_seed": [float(x) for x in v]}
+        out[key] = c
+    return out
+
+
 def main_mh_matrix():
     if not os.path.exists(HARNESS):
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
@@ -160,11 +206,13 @@ def main_mh_matrix():
     tmp = tempfile.mkdtemp(prefix="golden_mh_")
     try:
         mm = mh_matrix(tmp, z["off"], z["adj"])
+        ms = mh_stream_matrix(tmp, z["off"], z["adj"])
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     path = os.path.join(HERE, "golden.json")
     meta = json.load(open(path))
     meta["mh_matrix_reference"] = mm
+    meta["mh_stream_matrix_reference"] = ms
     with open(path, "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print("mh_matrix_reference written to", path)
@@ -312,6 +360,7 @@ def main():
             mh[f"{model}_p{p}_q{q}"] = st
         meta["mh_stats_reference"] = mh
         meta["mh_matrix_reference"] = mh_matrix(tmp, woff, wadj)
+        meta["mh_stream_matrix_reference"] = mh_stream_matrix(tmp, woff, wadj)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     with open(os.path.join(HERE, "golden.json"), "w") as f:

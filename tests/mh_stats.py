@@ -75,3 +75,14 @@ def check_cell(ref_cell: dict, ours: np.ndarray, label: str) -> list[str]:
         if abs(z) > Z_TOL:
             bad.append(f"{label} {cl}: ours {mu[i]:.5f} ref {rm:.5f} (sd {rs:.5f}) z={z:.1f}")
     return bad
+
+
+def stream_batches(matrix: dict, n: int, seed: int, gen_batch):
+    """The (insert?, pairs) batches of mh_stream_matrix_reference for one seed;
+    gen_batch = generate_batch_of_edges(edges, n, seed, self_loops, directed)."""
+    return [(b["insert"], gen_batch(b["edges"], n, seed + b["seed_offset"], False, False)) for b in matrix["batches"]]
+
+
+def stream_cells(matrix: dict):
+    return [(k, float(k.split("_")[1][1:]), float(k.split("_")[2][1:]), k.split("_")[3])
+            for k in sorted(matrix) if k.startswith("node2vec_")]

@@ -458,6 +458,45 @@ def test_mh_matrix_vs_reference(W, cell):
     assert not bad, bad
 
 
+_STREAM = json.load(open(os.path.join(G, "golden.json")))["mh_stream_matrix_reference"]
+
+
+@pytest.mark.parametrize("cell", mh_stats.stream_cells(_STREAM), ids=lambda c: c[0])
+def test_mh_stream_vs_reference(W, cell):
+    """MH re-walks through an insert and a delete batch on wiki (the reference's
+    MH update path, wharfmh.h:439-923, sampler resets of batch sources): class
+    fractions of the final corpus on the final graph against the reference's 8
+    seeds (`mh_stream_matrix_reference`); the first seed also bit-exact against
+    the oracle."""
+    key, p, q, init = cell
+    z = np.load(os.path.join(G, "wiki_csr.npz"))
+    off, adj = z["off"], z["adj"]
+    n = len(off) - 1
+    inits = {"random": 0, "burnin": 1, "weight": 2}
+    ours = []
+    for s in _STREAM["seeds"]:
+        cfg = W.WharfConfig(walks_per_vertex=_STREAM["wpv"], walk_length=_STREAM["L"], model=W.NODE2VEC,
+                            paramP=p, paramQ=q, sampler_init=inits[init], deterministic=False, seed=s)
+        g = W.WharfMH.from_csr(off, adj, config=cfg)
+        g.generate_initial_random_walks()
+        batches = mh_stats.stream_batches(_STREAM, n, s, O.generate_batch_of_edges)
+        for ins, b in batches:
+            (g.insert_edges_batch if ins else g.delete_edges_batch)(b, remove_dups=True)
+        o2, a2 = g.flatten_graph()
+        w = g.walks()
+        if s == _STREAM["seeds"][0]:
+            ref = O.Engine(off, adj, wpv=_STREAM["wpv"], L=_STREAM["L"], model=O.NODE2VEC, p=p, q=q,
+                           init=inits[init], deterministic=False, seed=s)
+            ref.generate()
+            for ins, b in batches:
+                ref.update(ins, b)
+            np.testing.assert_array_equal(w, ref.walks())
+        ours.append(mh_stats.class_fractions(w, o2, a2))
+        g.destroy()
+    bad = mh_stats.check_cell(_STREAM[key], np.array(ours), key)
+    assert not bad, bad
+
+
 # ---------------------------------------------------------------------------
 # full-size properties (no oracle needed)
 # ---------------------------------------------------------------------------

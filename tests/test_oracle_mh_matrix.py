@@ -47,3 +47,27 @@ def test_oracle_mh_cell_vs_reference(wiki, cell):
         ours.append(S.class_fractions(e.walks(), off, adj))
     bad = S.check_cell(MATRIX[key], np.array(ours), key)
     assert not bad, bad
+
+
+STREAM = json.load(open(os.path.join(G, "golden.json")))["mh_stream_matrix_reference"]
+
+
+@pytest.mark.parametrize("cell", S.stream_cells(STREAM), ids=lambda c: c[0])
+def test_oracle_mh_stream_vs_reference(wiki, cell):
+    """After an insert and a delete batch (re-walks, sampler resets of batch
+    sources): class fractions of the final corpus on the final graph, against
+    the reference's 8 seeds (`mh_stream_matrix_reference`)."""
+    key, p, q, init = cell
+    off, adj = wiki
+    n = len(off) - 1
+    ours = []
+    for s in STREAM["seeds"]:
+        e = O.Engine(off, adj, wpv=STREAM["wpv"], L=STREAM["L"], model=O.NODE2VEC, p=p, q=q, init=INITS[init],
+                     deterministic=False, seed=s)
+        e.generate()
+        for ins, b in S.stream_batches(STREAM, n, s, O.generate_batch_of_edges):
+            e.update(ins, b)
+        o2, a2 = e.csr()
+        ours.append(S.class_fractions(e.walks(), o2, a2))
+    bad = S.check_cell(STREAM[key], np.array(ours), key)
+    assert not bad, bad
