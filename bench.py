@@ -12,12 +12,19 @@ the replicated CSR and owns a contiguous start-vertex range of the walks
 A "step" = one generate_initial_random_walks() over the whole graph (all
 ranks' shards).  value = transitions appended by all ranks per second.
 
-Scaling (--scaling, default weak): every rank keeps the configs[1] per-GPU
-workload (4.19 M start vertices x 10 walks x 80): at N ranks the replicated RMAT
-graph has scale 22 + log2 N and N x 117 M undirected samples (N = 8: scale 25,
-~1.9 G CSR entries, the configs[3] twitter size), and rank g walks from its own
-start-vertex range.  --scaling strong keeps the scale-22 graph and splits its
-walks N ways.
+Scaling (--scaling, default weak): every rank keeps configs[1]'s per-GPU
+workload ON configs[1]'s graph: the scale-22 RMAT graph is replicated, the
+job generates 10 x N walks per vertex (rank g owns the start-vertex range g of
+N, i.e. 4.19 M / N vertices x 10 N rounds = configs[1]'s 41.9 M walks), so the
+per-GPU work and the graph stay configs[1]'s as N grows.  At N > 1 the line
+also carries `strong_scaling`: configs[1] exactly (10 walks per vertex) split N
+ways, value = its transitions / max-over-ranks time.  --scaling strong makes
+that the headline.
+
+Sub-records on rank 0 (same run): `mh_node2vec` (configs[4]'s model, p=.5
+q=2 WEIGHT, on the configs[1] graph: first and warm generation, a configs[2]
+re-walk stream), `rewalk_latency_10k_batch[_deterministic]` (configs[2]) and
+`streaming_rooflines` (rewalk-point scan, deterministic suffix copy, CSR move).
 """
 from __future__ import annotations
 
@@ -70,6 +77,8 @@ def parse():
     p.add_argument("--cpu-length", type=int, default=24,
                    help="walk length of the bounded reference CPU sample (~15-25 s on 16 host threads)")
     p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    p.add_argument("--n2v-steps", type=int, default=3, help="node2vec warm generations of the mh_node2vec record (0 = off)")
+    p.add_argument("--n2v-rewalk-batches", type=int, default=5, help="configs[2] batches of the mh_node2vec record")
     return p.parse_args()
 
 
@@ -171,7 +180,7 @@ def cpu_baseline(args, n, active_vertices, off, adj, kind):
                       f"{steps} steps in {secs:.2f} s", "seconds": secs}
 
 
-def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrier, batches):
+def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrier, batches, scan_batches=0):
     """configs[2]: per-batch latency of 10k-edge insert batches with the re-walk applied
     (memory-throughput-latency.cpp:126-134: generate_batch_of_edges(5000, n, seed=b, false, undirected))."""
     if batches <= 0:
@@ -186,7 +195,7 @@ def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrie
     # affected walk ids stay in HBM (WHARF_AFFECTED_DEVICE); the host-list
     # variant (PCIe-inclusive, the reference's return value) is timed after
     out = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
-    lat, aff, gu, wu, kern, rsteps = [], [], [], [], [], []
+    lat, aff, gu, wu, kern, rsteps, mv, mslots = [], [], [], [], [], [], [], []
     for b in range(batches):
         batch = W.generate_batch_of_edges(5000, ns, b, False, False, device=dev)
         barrier()
@@ -200,6 +209,14 @@ def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrie
         wu.append(s2["last_walk_update_ms"])
         kern.append(s2["last_walk_kernel_ms"])
         rsteps.append(s2["steps"])
+        mv.append(s2["last_csr_move_ms"])
+        mslots.append(s2["last_moved_slots"])
+    # rewalk points alone (apply_walk_updates = false): the scan over the whole walk matrix
+    scan = []
+    for b in range(scan_batches):
+        batch = W.generate_batch_of_edges(5000, ns, 10_000 + b, False, False, device=dev)
+        gs.insert_edges_batch(batch, remove_dups=True, apply_walk_updates=False, out=out)
+        scan.append(gs.stats()["last_walk_kernel_ms"])
     hout = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, pin_memory=True).numpy().view(np.uint32)
     lat_host = []
     for b in range(batches, batches + min(5, batches)):
@@ -227,11 +244,104 @@ def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrie
            "median_rewalk_kernel_ms": round(float(np.median(kern)), 3),
            "mean_rewalk_steps_rank0": int(np.mean(rsteps)),
            "rewalk_Gsteps_per_s": round(float(np.sum(rsteps) / np.sum(kern) / 1e6), 2),
-           "generation_same_graph": gen3}
+           "generation_same_graph": gen3,
+           "median_csr_move_ms": round(float(np.median(mv)), 4), "moved_slots": int(np.median(mslots)),
+           "stored_positions_rank0": int(gs.number_of_walks) * args.length,
+           "record_bytes": 32 if (cfg.model == W.NODE2VEC and not cfg.deterministic) else 16}
+    if scan:
+        res["scan_only_median_ms"] = round(float(np.median(scan)), 4)
     gs.destroy()
     return res
 
 
+
+
+def timed_generation(g, steps, warmup, barrier, log_rank=None):
+    """W untimed + K timed generate_initial_random_walks(), barrier + sync on both
+    sides.  Returns (elapsed s, per-launch kernel ms of the timed steps, warmup ms)."""
+    warm_ms = []
+    for i in range(warmup):
+        g.generate_initial_random_walks()
+        warm_ms.append(g.stats()["last_walk_kernel_ms"])
+        if log_rank is not None:
+            log(f"[rank {log_rank}] warmup {i}: {warm_ms[-1]:.1f} ms")
+    barrier()
+    t_start = time.perf_counter()
+    kern_ms = []
+    for _ in range(steps):
+        g.generate_initial_random_walks()
+        kern_ms.append(g.stats()["last_walk_kernel_ms"])
+    barrier()
+    return time.perf_counter() - t_start, kern_ms, warm_ms
+
+
+def reduce_steps_time(torch, dist, comm_dev, steps_local, elapsed):
+    """(sum of transitions over ranks, max elapsed over ranks)"""
+    if not dist:
+        return steps_local, elapsed
+    tt = torch.tensor([float(steps_local), elapsed], dtype=torch.float64, device=comm_dev)
+    s = tt.clone()
+    dist.all_reduce(s, op=dist.ReduceOp.SUM)
+    mx = tt.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    return int(s[0].item()), mx[1].item()
+
+
+def node2vec_record(args, W, torch, dev, barrier, n):
+    """configs[4]'s model (node2vec p, q, WEIGHT inits, MH) on the configs[1] graph:
+    the first generation of a fresh handle (every anchor initialised), warm
+    generations (anchors cached), then configs[2]'s re-walk stream."""
+    cfg = W.WharfConfig(walks_per_vertex=args.wpv, walk_length=args.length, model=W.NODE2VEC, paramP=args.paramP,
+                        paramQ=args.paramQ, deterministic=False, seed=0x5EED)
+    g = W.WharfMH.from_rmat(n, args.samples, 2 * n, seed=args.seed, config=cfg, device=dev)
+    elapsed, kern, warm = timed_generation(g, args.n2v_steps, 1, barrier)
+    st = g.stats()
+    steps = st["steps"]
+    avg = float(np.mean(kern))
+    achieved = steps * BYTES_PER_STEP_NODE2VEC / (avg * 1e-3) / 1e9
+    rec = {"workload": f"configs[1] graph (RMAT scale {args.scale}, m={g.number_of_edges()}), node2vec "
+                       f"p={args.paramP} q={args.paramQ} MH, WEIGHT sampler init, walks_per_vertex={args.wpv}, "
+                       f"walk_length={args.length}",
+           "value": round(steps * len(kern) / elapsed, 1), "unit": "walk-steps/s",
+           "warm_generation_kernel_ms": round(avg, 3), "first_generation_kernel_ms": round(warm[0], 3),
+           "first_generation_Gsteps_per_s": round(steps / (warm[0] * 1e-3) / 1e9, 2),
+           "mh_accept_rate": round(st["accepts"] / steps, 5) if steps else None,
+           "roofline": {"bound": "hbm", "kernel": "k_walk<node2vec, MH> (warm generation)",
+                        "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 5), "bytes_per_step": BYTES_PER_STEP_NODE2VEC,
+                        "traffic": load_traffic(f"gen_node2vec_mh_s{args.scale}"),
+                        "traffic_source": f"profiles/pmc_gen_node2vec_mh_s{args.scale}.json (rocprofv3 PMC pass)"}}
+    g.destroy()
+    rec["rewalk_latency_10k_batch"] = stream_latency(args, W, torch, cfg, dev, 1, 0, None, None, barrier,
+                                                     args.n2v_rewalk_batches)
+    return rec
+
+
+def streaming_rooflines(rewalk, rewalk_det):
+    """The streaming kernels of the update path against the HBM peak, by
+    algorithmic bytes (SURVEY 8(d)): rewalk-point scan 4 B per stored position;
+    deterministic re-walk (suffix table + chunked copy) 4 B per stored position
+    (each position is read up to the walk's rewalk point and written after it);
+    CSR move 2 x (4 B target + record) per old slot."""
+    out = {}
+    def ent(kernel, bytes_, ms, per):
+        if not ms:
+            return None
+        a = bytes_ / (ms * 1e-3) / 1e9
+        return {"kernel": kernel, "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(a / HBM_PEAK_GBS, 4), "ms": ms, "algorithmic_bytes": int(bytes_), "per_unit": per}
+    if rewalk_det:
+        pos = rewalk_det["stored_positions_rank0"]
+        out["rewalk_point_scan"] = ent("k_rewalk_chunked<false> (apply_walk_updates=false)", 4 * pos,
+                                       rewalk_det.get("scan_only_median_ms"), "4 B per stored position")
+        out["deterministic_rewalk_copy"] = ent("k_det_suffix + k_rewalk_chunked<true>", 4 * pos,
+                                               rewalk_det["median_rewalk_kernel_ms"], "4 B per stored position")
+    src = rewalk or rewalk_det
+    if src:
+        per = 2 * (4 + src["record_bytes"])
+        out["csr_move"] = ent("k_move_edges (record patch into the second buffer)", per * src["moved_slots"],
+                              src["median_csr_move_ms"], f"{per} B per old CSR slot")
+    return out or None
 
 
 def main():
@@ -255,68 +365,50 @@ def main():
             dist.init_process_group(backend)
     import dynamicgraphrepresentationlearning_amd as W
 
-    # weak scaling: the replicated graph grows with the ranks so each rank keeps
-    # configs[1]'s per-GPU walk count (N = 2^k ranks: scale + k, samples x N)
-    grow = (max(world, 1) - 1).bit_length() if args.scaling == "weak" else 0
-    scale = args.scale + grow
-    samples = args.samples * (1 << grow)
-    n = 1 << scale
-    cfg = W.WharfConfig(walks_per_vertex=args.wpv, walk_length=args.length,
-                        model=W.NODE2VEC if args.model == "node2vec" else W.DEEPWALK,
+    # weak scaling: configs[1]'s graph, 10 x N walks per vertex, so each rank's
+    # start-vertex range carries configs[1]'s 41.9 M walks
+    weak = args.scaling == "weak"
+    wpv = args.wpv * world if weak else args.wpv
+    if wpv > 255:
+        raise SystemExit(f"walks_per_vertex {wpv} exceeds the reference's u8 config::walks_per_vertex")
+    n = 1 << args.scale
+    model = W.NODE2VEC if args.model == "node2vec" else W.DEEPWALK
+    cfg = W.WharfConfig(walks_per_vertex=wpv, walk_length=args.length, model=model,
                         paramP=args.paramP, paramQ=args.paramQ, deterministic=args.det, seed=0x5EED)
     t0 = time.time()
-    g = W.WharfMH.from_rmat(n, samples, 2 * n, seed=args.seed, config=cfg, device=dev)
+    g = W.WharfMH.from_rmat(n, args.samples, 2 * n, seed=args.seed, config=cfg, device=dev)
     # the whole CSR on the host only where the CPU baseline may need it (N = 1)
     off, adj = g.flatten_graph() if world == 1 else (g.offsets(), None)
     deg = np.diff(off.astype(np.int64))
-    lo, hi = balanced_shards(deg, world)[rank]
+    shards = balanced_shards(deg, world)
+    lo, hi = shards[rank]
     g.set_shard(lo, hi)
     m = g.number_of_edges()
-    log(f"[rank {rank}] graph n={n} m={m} built in {time.time() - t0:.1f}s; shard [{lo},{hi})")
+    log(f"[rank {rank}] graph n={n} m={m} built in {time.time() - t0:.1f}s; shard [{lo},{hi}), wpv={wpv}")
 
     def barrier():
         if dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    warm_ms = []
-    for i in range(args.warmup):
-        g.generate_initial_random_walks()
-        warm_ms.append(g.stats()["last_walk_kernel_ms"])
-        log(f"[rank {rank}] warmup {i}: {warm_ms[-1]:.1f} ms")
-    barrier()
-    t_start = time.perf_counter()
-    kern_ms = []
-    for i in range(args.steps):
-        g.generate_initial_random_walks()
-        kern_ms.append(g.stats()["last_walk_kernel_ms"])
-    barrier()
-    elapsed = time.perf_counter() - t_start
+    elapsed, kern_ms, warm_ms = timed_generation(g, args.steps, args.warmup, barrier, rank)
     st = g.stats()
     steps_local = st["steps"]
-    steps_total, t_max = steps_local, elapsed
-    if dist:
-        tt = torch.tensor([float(steps_local), elapsed], dtype=torch.float64, device=comm_dev)
-        s = tt.clone()
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        mx = tt.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        steps_total, t_max = int(s[0].item()), mx[1].item()
+    steps_total, t_max = reduce_steps_time(torch, dist, comm_dev, steps_local, elapsed)
     value = steps_total * args.steps / t_max
     avg_kernel_ms = float(np.mean(kern_ms))
     bytes_per_step = BYTES_PER_STEP_DEEPWALK if args.model == "deepwalk" or args.det else BYTES_PER_STEP_NODE2VEC
-    tag = f"gen_{args.model}_{'det' if args.det else 'mh'}_s{scale}"
+    tag = f"gen_{args.model}_{'det' if args.det else 'mh'}_s{args.scale}"
 
     # corpus reassembly for the downstream consumer: full-mesh all-gatherv over RCCL (not timed in `value`)
     corpus = None
     if dist:
         from dynamicgraphrepresentationlearning_amd.distributed import allgatherv_corpus
-        shards = balanced_shards(deg, world)
         loc = torch.empty((g.number_of_walks, args.length), dtype=torch.int32, device=f"cuda:{dev}")
         g.export_walks_device(loc.data_ptr(), layout="walk")
         # the whole corpus on every rank, or its first rounds when it would not fit
-        # beside the graph (weak scaling at N = 8: a 107 GB corpus); local rows are round-major
-        rounds = max(1, min(args.wpv, (16 << 30) // max(n * args.length * 4, 1)))
+        # beside the graph (<= 16 GiB); local rows are round-major
+        rounds = max(1, min(wpv, (16 << 30) // max(n * args.length * 4, 1)))
         loc = loc[: (hi - lo) * rounds].to(comm_dev)
         barrier()
         t1 = time.perf_counter()
@@ -324,21 +416,40 @@ def main():
         barrier()
         gms = (time.perf_counter() - t1) * 1e3
         recv = full.numel() * 4 - loc.numel() * 4
-        corpus = {"ms": round(gms, 3), "rounds": rounds, "bytes_received_per_rank": int(recv),
+        corpus = {"ms": round(gms, 3), "rounds": rounds, "of_rounds": wpv, "bytes_received_per_rank": int(recv),
                   "GBps_per_rank": round(recv / gms / 1e6, 1), "pattern": "batch_isend_irecv full mesh"}
         del full, loc
-
     g.destroy()
+
+    # strong scaling beside the weak line: configs[1] exactly (10 walks per vertex) split N ways
+    strong = None
+    if world > 1 and weak:
+        cfg1 = W.WharfConfig(walks_per_vertex=args.wpv, walk_length=args.length, model=model,
+                             paramP=args.paramP, paramQ=args.paramQ, deterministic=args.det, seed=0x5EED)
+        g1 = W.WharfMH.from_rmat(n, args.samples, 2 * n, seed=args.seed, config=cfg1, device=dev)
+        g1.set_shard(lo, hi)
+        e1, k1, _ = timed_generation(g1, args.steps, 1, barrier)
+        st1, tm1 = reduce_steps_time(torch, dist, comm_dev, g1.stats()["steps"], e1)
+        strong = {"workload": f"configs[1] exactly (walks_per_vertex={args.wpv}) split over {world} ranks",
+                  "value": round(st1 * args.steps / tm1, 1), "unit": "walk-steps/s",
+                  "ms_per_step": round(tm1 / args.steps * 1e3, 3), "transitions_per_step": st1,
+                  "avg_kernel_ms_rank0": round(float(np.mean(k1)), 3)}
+        g1.destroy()
 
     # configs[2]: soc-LiveJournal-sized streaming, 10k-edge insert batches, in the
     # benchmarked mode and (DeepWalk MH runs) in deterministic mode, the reference's default
-    rewalk = stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrier, args.rewalk_batches)
+    cfg2 = W.WharfConfig(walks_per_vertex=args.wpv, walk_length=args.length, model=model,
+                         paramP=args.paramP, paramQ=args.paramQ, deterministic=args.det, seed=0x5EED)
+    rewalk = stream_latency(args, W, torch, cfg2, dev, world, rank, dist, comm_dev, barrier, args.rewalk_batches)
     rewalk_det = None
     if args.det_rewalk_batches > 0 and not args.det and args.model == "deepwalk":
         cfg_det = W.WharfConfig(walks_per_vertex=args.wpv, walk_length=args.length, model=W.DEEPWALK,
                                 deterministic=True)
         rewalk_det = stream_latency(args, W, torch, cfg_det, dev, world, rank, dist, comm_dev, barrier,
-                                    args.det_rewalk_batches)
+                                    args.det_rewalk_batches, scan_batches=3)
+    n2v = None
+    if world == 1 and args.model == "deepwalk" and not args.det and args.n2v_steps > 0:
+        n2v = node2vec_record(args, W, torch, dev, barrier, n)
 
     if rank == 0:
         live_ceiling = measure_gather_ceiling() if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None
@@ -360,25 +471,30 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic RMAT (utility::generate_batch_of_edges semantics, a=.5 b=.2 c=.1), built on device",
-            "config": {"workload": f"configs[1] com-orkut-sized initial walk generation"
-                                   f"{' per GPU (weak scaling)' if grow else ''}: RMAT scale {scale} "
-                                   f"(n={n}), {samples} undirected samples (seed {args.seed}) -> m={m} CSR "
+            "config": {"workload": f"configs[1] com-orkut-sized initial walk generation: RMAT scale {args.scale} "
+                                   f"(n={n}), {args.samples} undirected samples (seed {args.seed}) -> m={m} CSR "
                                    f"entries; {args.model} {'deterministic' if args.det else 'MH'}, "
-                                   f"walks_per_vertex={args.wpv}, walk_length={args.length}",
-                       "n": n, "m": m, "walks": n * args.wpv, "transitions_per_step": steps_total,
+                                   f"walks_per_vertex={wpv}"
+                                   f"{f' ({args.wpv} per GPU x {world}: weak scaling)' if weak and world > 1 else ''}"
+                                   f", walk_length={args.length}",
+                       "n": n, "m": m, "walks": n * wpv, "transitions_per_step": steps_total,
                        "parallelism": f"walk shards by start-vertex range x{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_walk (generation)",
                          "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
-                         "traffic": traffic, "bytes_per_step": bytes_per_step,
+                         "traffic": traffic, "traffic_source": f"profiles/pmc_{tag}.json (rocprofv3 PMC pass)",
+                         "bytes_per_step": bytes_per_step,
                          "avg_kernel_ms": round(avg_kernel_ms, 3),
                          # the first generation of a fresh handle (node2vec: every anchor initialised)
                          "first_generation_kernel_ms": round(warm_ms[0], 3) if warm_ms else None,
                          "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3), live_ceiling)
                          if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None},
             "mh_accept_rate": round(st["accepts"] / st["steps"], 5) if st["steps"] else None,
+            "strong_scaling": strong,
+            "mh_node2vec": n2v,
             "rewalk_latency_10k_batch": rewalk,
             "rewalk_latency_10k_batch_deterministic": rewalk_det,
+            "streaming_rooflines": streaming_rooflines(rewalk, rewalk_det),
             "corpus_allgatherv": corpus,
             "cpu_baseline": None,
         }

@@ -59,6 +59,8 @@ class wharf_stats(C.Structure):
         ("last_total_ms", C.c_double),
         ("hbm_bytes_walks", C.c_uint64),
         ("hbm_bytes_graph", C.c_uint64),
+        ("last_csr_move_ms", C.c_double),
+        ("last_moved_slots", C.c_uint64),
     ]
 
 

@@ -78,7 +78,7 @@ uint32_t bits_for(uint64_t x)   // bits needed to represent values < x
 struct wharf_handle {
     int device = 0;
     hipStream_t s = nullptr;
-    hipEvent_t ev[4] = {};
+    hipEvent_t ev[6] = {};
     wharf_config cfg{};
     uint64_t n = 0, m = 0, lo = 0, hi = 0, n_loc = 0, W = 0;
     uint32_t L = 0, wpv = 0;
@@ -421,6 +421,8 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->st.batch_edges = 0;
         h->st.steps = h->st.accepts = 0;
         h->st.last_graph_update_ms = h->st.last_walk_update_ms = h->st.last_walk_kernel_ms = 0;
+        h->st.last_csr_move_ms = 0;
+        h->st.last_moved_slots = 0;
         if (n_affected) *n_affected = 0;
         if (m == 0) return;
         hipStream_t s = h->s;
@@ -524,10 +526,13 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
                             : path == kPatch ? h->erec2.as<uint64_t>() + 2 : h->anchor2.as<uint64_t>();
         const uint32_t as_out = path == kPatch ? (uint32_t)kAnchorStride : 1u;
         const uint64_t m_old = h->m;
+        HIPCHK(hipEventRecord(h->ev[4], s));
         launch_move_edges(h->adj.as<uint32_t>(), anc_in, kAnchorStride, m_old, rx, bkeys, h->cf.as<uint32_t>(),
                           h->off2.as<uint64_t>(), insert, h->adj2.as<uint32_t>(), anc_out, as_out, m_new,
                           path == kPatch ? h->erec.as<ERec>() : nullptr, path == kPatch ? h->erec2.as<ERec>() : nullptr,
                           (uint32_t)rs, mb, h->epoch, s);
+        HIPCHK(hipEventRecord(h->ev[5], s));
+        h->st.last_moved_slots = m_old;
         if (insert)   // (the records of source rows, new slots included, are rebuilt below)
             launch_place_new(bkeys, mb, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(), h->runstart.as<uint32_t>(), k,
                              h->runs.as<RunInfo>(), h->adj.as<uint32_t>(), h->off2.as<uint64_t>(),
@@ -629,6 +634,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             h->sync();
         }
         h->st.last_graph_update_ms = h->elapsed(0, 1);
+        h->st.last_csr_move_ms = h->elapsed(4, 5);
         h->st.last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
 }

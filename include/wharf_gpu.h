@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define WHARF_ABI_VERSION 1
+#define WHARF_ABI_VERSION 2
 
 enum {
     WHARF_OK = 0,
@@ -78,6 +78,8 @@ typedef struct wharf_stats {
     double   last_total_ms;        /* host wall time of the last call */
     uint64_t hbm_bytes_walks;      /* resident bytes: walk matrix */
     uint64_t hbm_bytes_graph;      /* resident bytes: CSR + vertex records (+ anchors) */
+    double   last_csr_move_ms;     /* device time of the last update's streaming CSR pass (k_move_edges) */
+    uint64_t last_moved_slots;     /* old CSR slots that pass read (the old m) */
 } wharf_stats;
 
 typedef struct wharf_handle wharf_handle;
