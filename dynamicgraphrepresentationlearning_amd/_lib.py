@@ -97,6 +97,8 @@ SIGNATURES = {
     "wharf_walk_ids": (_I, [_P, _P]),
     "wharf_index_size": (_I, [_P, _P]),
     "wharf_export_index": (_I, [_P, _P, _P, _P]),
+    "wharf_index_size_range": (_I, [_P, C.c_uint64, C.c_uint64, _P]),
+    "wharf_export_index_range": (_I, [_P, C.c_uint64, C.c_uint64, _P, _P, _P]),
     "wharf_get_stats": (_I, [_P, _P]),
     "wharf_export_index_paired": (_I, [_P, _P, _P]),
     "wharf_memory_footprint": (_I, [_P, _P]),

@@ -969,21 +969,22 @@ int wharf_walk_ids(wharf_handle* h, uint32_t* ids)
 }
 
 namespace {
-// Builds the inverted index of this handle's walks, sorted by (vertex, key);
-// returns the entry count.  Leaves sort keys in k1 and values in k2.
-uint64_t build_index(wharf_handle* h, int& kb)
+// Builds the inverted index of this handle's walks for the vertices of
+// [v0, v1), sorted by (vertex, key); returns the entry count.  Leaves the
+// sorted keys (vertex - v0) << kb | key in k2 and their values in pairs.
+uint64_t build_index(wharf_handle* h, int& kb, uint64_t v0, uint64_t v1)
 {
     const uint64_t W = h->W;
     h->ensure_walks();
     kb = (int)std::max<uint32_t>(bits_for(h->n * h->wpv * h->L), 1);
-    const int vb = (int)std::max<uint32_t>(bits_for(h->n), 1);
+    const int vb = (int)std::max<uint32_t>(bits_for(v1 - v0), 1);
     REQUIRE(kb + vb <= 64, WHARF_E_INVALID, "index key does not fit 64 bits");
     h->sel.ensure((W + 1) * 8);
     h->count.ensure((W + 1) * 8);
     uint64_t* len = h->sel.as<uint64_t>();
     uint64_t* base = h->count.as<uint64_t>();
     HIPCHK(hipMemsetAsync(len + W, 0, 8, h->s));
-    launch_walk_lengths(h->walks.as<uint32_t>(), W, h->L, len, h->s);
+    launch_walk_lengths(h->walks.as<uint32_t>(), W, h->L, (uint32_t)v0, (uint32_t)v1, len, h->s);
     h->rp([&](void* t, size_t& b) {
         return rocprim::exclusive_scan(t, b, len, base, (uint64_t)0, (size_t)(W + 1), rocprim::plus<uint64_t>(), h->s);
     });
@@ -995,8 +996,8 @@ uint64_t build_index(wharf_handle* h, int& kb)
     h->k2.ensure(E * 8);
     h->flags.ensure(E * 4);
     h->pairs.ensure(E * 4);
-    launch_index_entries(h->walks.as<uint32_t>(), W, h->L, h->n, h->n_loc, h->lo, kb, base, h->k1.as<uint64_t>(),
-                         h->flags.as<uint32_t>(), h->s);
+    launch_index_entries(h->walks.as<uint32_t>(), W, h->L, h->n, h->n_loc, h->lo, kb, (uint32_t)v0, (uint32_t)v1, base,
+                         h->k1.as<uint64_t>(), h->flags.as<uint32_t>(), h->s);
     uint64_t* ki = h->k1.as<uint64_t>();
     uint64_t* ko = h->k2.as<uint64_t>();
     uint32_t* vi = h->flags.as<uint32_t>();
@@ -1005,19 +1006,19 @@ uint64_t build_index(wharf_handle* h, int& kb)
     h->rp([&](void* t, size_t& b) { return rocprim::radix_sort_pairs(t, b, ki, ko, vi, vo, (size_t)E, 0u, eb, h->s); });
     return E;
 }
-}  // namespace
 
-int wharf_index_size(wharf_handle* h, uint64_t* size)
+int index_size(wharf_handle* h, uint64_t v0, uint64_t v1, uint64_t* size)
 {
     return guarded(h, [&] {
         REQUIRE(h && size, WHARF_E_INVALID, "null argument");
+        REQUIRE(v0 <= v1 && v1 <= h->n, WHARF_E_INVALID, "vertex window out of range");
         h->ensure_walks();
         h->sel.ensure((h->W + 1) * 8);
         h->count.ensure((h->W + 1) * 8);
         uint64_t* len = h->sel.as<uint64_t>();
         uint64_t* base = h->count.as<uint64_t>();
         HIPCHK(hipMemsetAsync(len + h->W, 0, 8, h->s));
-        launch_walk_lengths(h->walks.as<uint32_t>(), h->W, h->L, len, h->s);
+        launch_walk_lengths(h->walks.as<uint32_t>(), h->W, h->L, (uint32_t)v0, (uint32_t)v1, len, h->s);
         h->rp([&](void* t, size_t& b) {
             return rocprim::exclusive_scan(t, b, len, base, (uint64_t)0, (size_t)(h->W + 1), rocprim::plus<uint64_t>(), h->s);
         });
@@ -1026,24 +1027,45 @@ int wharf_index_size(wharf_handle* h, uint64_t* size)
     });
 }
 
-int wharf_export_index(wharf_handle* h, uint64_t* counts, uint64_t* keys, uint32_t* nexts)
+int export_index(wharf_handle* h, uint64_t v0, uint64_t v1, uint64_t* counts, uint64_t* keys, uint32_t* nexts)
 {
     return guarded(h, [&] {
         REQUIRE(h && counts, WHARF_E_INVALID, "null argument");
+        REQUIRE(v0 <= v1 && v1 <= h->n, WHARF_E_INVALID, "vertex window out of range");
+        const uint64_t nv = v1 - v0;
         int kb = 0;
-        const uint64_t E = build_index(h, kb);
-        h->runs.ensure(h->n * 8);
-        HIPCHK(hipMemsetAsync(h->runs.p, 0, h->n * 8, h->s));
+        const uint64_t E = nv ? build_index(h, kb, v0, v1) : 0;
+        h->runs.ensure(std::max<uint64_t>(nv, 1) * 8);
+        HIPCHK(hipMemsetAsync(h->runs.p, 0, std::max<uint64_t>(nv, 1) * 8, h->s));
         if (E) {
             REQUIRE(keys && nexts, WHARF_E_INVALID, "null argument");
-            // k2 holds sorted (vertex<<kb | key); split into counts and keys (reuse k1)
+            // k2 holds sorted ((vertex - v0) << kb | key); split into counts and keys (reuse k1)
             launch_index_split(h->k2.as<uint64_t>(), E, kb, h->runs.as<unsigned long long>(), h->k1.as<uint64_t>(), h->s);
             HIPCHK(hipMemcpyAsync(keys, h->k1.p, E * 8, hipMemcpyDeviceToHost, h->s));
             HIPCHK(hipMemcpyAsync(nexts, h->pairs.p, E * 4, hipMemcpyDeviceToHost, h->s));
         }
-        HIPCHK(hipMemcpyAsync(counts, h->runs.p, h->n * 8, hipMemcpyDeviceToHost, h->s));
+        if (nv) HIPCHK(hipMemcpyAsync(counts, h->runs.p, nv * 8, hipMemcpyDeviceToHost, h->s));
         h->sync();
     });
+}
+}  // namespace
+
+int wharf_index_size(wharf_handle* h, uint64_t* size) { return index_size(h, 0, h ? h->n : 0, size); }
+
+int wharf_index_size_range(wharf_handle* h, uint64_t v0, uint64_t v1, uint64_t* size)
+{
+    return index_size(h, v0, v1, size);
+}
+
+int wharf_export_index(wharf_handle* h, uint64_t* counts, uint64_t* keys, uint32_t* nexts)
+{
+    return export_index(h, 0, h ? h->n : 0, counts, keys, nexts);
+}
+
+int wharf_export_index_range(wharf_handle* h, uint64_t v0, uint64_t v1, uint64_t* counts, uint64_t* keys,
+                             uint32_t* nexts)
+{
+    return export_index(h, v0, v1, counts, keys, nexts);
 }
 
 int wharf_export_index_paired(wharf_handle* h, uint64_t* counts, uint64_t* paired)
@@ -1051,7 +1073,7 @@ int wharf_export_index_paired(wharf_handle* h, uint64_t* counts, uint64_t* paire
     return guarded(h, [&] {
         REQUIRE(h && counts, WHARF_E_INVALID, "null argument");
         int kb = 0;
-        const uint64_t E = build_index(h, kb);
+        const uint64_t E = build_index(h, kb, 0, h->n);
         const uint64_t n = h->n;
         h->runs.ensure(n * 8);
         HIPCHK(hipMemsetAsync(h->runs.p, 0, n * 8, h->s));

@@ -117,9 +117,11 @@ void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out,
 void launch_gather_walk(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* out, hipStream_t s);
 void launch_gather_rows(const uint32_t* walks, uint64_t W, uint32_t L, const uint64_t* list, uint64_t base,
                         uint64_t count, uint32_t* out, hipStream_t s);
-void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t* len, hipStream_t s);
-void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc, uint64_t lo,
-                          int kb, const uint64_t* col_base, uint64_t* skeys, uint32_t* vals, hipStream_t s);
+void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint32_t v0, uint32_t v1, uint64_t* len,
+                         hipStream_t s);
+void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc, uint64_t lo, int kb,
+                          uint32_t v0, uint32_t v1, const uint64_t* col_base, uint64_t* skeys, uint32_t* vals,
+                          hipStream_t s);
 void launch_index_split(const uint64_t* skeys, uint64_t E, int kb, unsigned long long* counts, uint64_t* keys,
                         hipStream_t s);
 unsigned aff_blocks(uint64_t W);

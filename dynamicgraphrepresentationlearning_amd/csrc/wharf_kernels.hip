@@ -1728,8 +1728,11 @@ void launch_gather_rows(const uint32_t* walks, uint64_t W, uint32_t L, const uin
 }
 
 // entries: sort key = (vertex << kb) | (wid*L + pos), value = next
+// Index entries of the vertices in the window [v0, v1): sort key
+// (v - v0) << kb | (wid * L + p) (64-bit: n * wpv * L may exceed 2^32),
+// value = the next vertex.  The whole index is the window [0, n).
 __global__ void k_index_entries(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc,
-                                uint64_t lo, int kb, const uint64_t* __restrict__ col_base,
+                                uint64_t lo, int kb, uint32_t v0, uint32_t v1, const uint64_t* __restrict__ col_base,
                                 uint64_t* __restrict__ skeys, uint32_t* __restrict__ vals)
 {
     for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += (uint64_t)gridDim.x * blockDim.x) {
@@ -1739,21 +1742,25 @@ __global__ void k_index_entries(const uint32_t* __restrict__ walks, uint64_t W, 
         for (uint32_t p = 0; p < L; p++) {
             const uint32_t v = walks[(uint64_t)p * W + li];
             if (v == kSent) break;
+            if (v < v0 || v >= v1) continue;
             const uint32_t nx = p + 1 < L ? walks[(uint64_t)(p + 1) * W + li] : kSent;
-            skeys[at] = ((uint64_t)v << kb) | (wid * L + p);
+            skeys[at] = ((uint64_t)(v - v0) << kb) | (wid * L + p);
             vals[at] = nx;
             at++;
         }
     }
 }
 
-__global__ void k_walk_lengths(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, uint64_t* __restrict__ len)
+// per walk: its positions holding a vertex of [v0, v1)
+__global__ void k_walk_lengths(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, uint32_t v0, uint32_t v1,
+                               uint64_t* __restrict__ len)
 {
     for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t c = 0;
         for (uint32_t p = 0; p < L; p++) {
-            if (walks[(uint64_t)p * W + li] == kSent) break;
-            c++;
+            const uint32_t v = walks[(uint64_t)p * W + li];
+            if (v == kSent) break;
+            c += v >= v0 && v < v1;
         }
         len[li] = c;
     }
@@ -1970,11 +1977,13 @@ void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out,
 }
 void launch_gather_walk(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* out, hipStream_t s)
 { hipLaunchKernelGGL(k_gather_walk, 1, 256, 0, s, walks, W, L, li, out); }
-void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t* len, hipStream_t s)
-{ hipLaunchKernelGGL(k_walk_lengths, grid_for(W, 256), 256, 0, s, walks, W, L, len); }
+void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint32_t v0, uint32_t v1, uint64_t* len,
+                         hipStream_t s)
+{ hipLaunchKernelGGL(k_walk_lengths, grid_for(W, 256), 256, 0, s, walks, W, L, v0, v1, len); }
 void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc, uint64_t lo, int kb,
-                          const uint64_t* col_base, uint64_t* skeys, uint32_t* vals, hipStream_t s)
-{ hipLaunchKernelGGL(k_index_entries, grid_for(W, 256), 256, 0, s, walks, W, L, n, n_loc, lo, kb, col_base, skeys, vals); }
+                          uint32_t v0, uint32_t v1, const uint64_t* col_base, uint64_t* skeys, uint32_t* vals,
+                          hipStream_t s)
+{ hipLaunchKernelGGL(k_index_entries, grid_for(W, 256), 256, 0, s, walks, W, L, n, n_loc, lo, kb, v0, v1, col_base, skeys, vals); }
 void launch_index_split(const uint64_t* skeys, uint64_t E, int kb, unsigned long long* counts, uint64_t* keys, hipStream_t s)
 { hipLaunchKernelGGL(k_index_split, grid_for(E, 256), 256, 0, s, skeys, E, kb, counts, keys); }
 void launch_fill_u64(uint64_t* p, uint64_t cnt, uint64_t v, hipStream_t s)

@@ -274,16 +274,27 @@ class WharfMH:
             rc = L.lib.wharf_write_corpus(self._h, path.encode(), _ptr(ids), len(ids), int(append))
         L.check(rc, self._h, "write_corpus")
 
-    def inverted_index(self):
+    def inverted_index(self, v0: int | None = None, v1: int | None = None):
         """Per-vertex ascending (key = wid*L + pos, next) lists (walks/inverted_index.h):
-        returns (counts[n], keys, nexts)."""
+        returns (counts, keys, nexts) for every vertex, or for the vertex window
+        [v0, v1) only (counts[v1 - v0]).  Keys are 64-bit."""
         sz = C.c_uint64()
-        L.check(L.lib.wharf_index_size(self._h, C.byref(sz)), self._h, "index_size")
-        n = self.number_of_vertices()
-        counts = np.zeros(n, dtype=np.uint64)
+        if v0 is None and v1 is None:
+            L.check(L.lib.wharf_index_size(self._h, C.byref(sz)), self._h, "index_size")
+            counts = np.zeros(self.number_of_vertices(), dtype=np.uint64)
+        else:
+            v0 = 0 if v0 is None else v0
+            v1 = self.number_of_vertices() if v1 is None else v1
+            L.check(L.lib.wharf_index_size_range(self._h, v0, v1, C.byref(sz)), self._h, "index_size_range")
+            counts = np.zeros(max(v1 - v0, 1), dtype=np.uint64)
         keys = np.zeros(max(sz.value, 1), dtype=np.uint64)
         nexts = np.zeros(max(sz.value, 1), dtype=np.uint32)
-        L.check(L.lib.wharf_export_index(self._h, _ptr(counts), _ptr(keys), _ptr(nexts)), self._h, "export_index")
+        if v0 is None and v1 is None:
+            L.check(L.lib.wharf_export_index(self._h, _ptr(counts), _ptr(keys), _ptr(nexts)), self._h, "export_index")
+        else:
+            L.check(L.lib.wharf_export_index_range(self._h, v0, v1, _ptr(counts), _ptr(keys), _ptr(nexts)), self._h,
+                    "export_index_range")
+            counts = counts[: v1 - v0]
         return counts, keys[: sz.value], nexts[: sz.value]
 
     def compressed_walks(self):

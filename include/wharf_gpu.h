@@ -165,6 +165,14 @@ int wharf_walk_ids(wharf_handle* h, uint32_t* ids_out);
 int wharf_index_size(wharf_handle* h, uint64_t* size);
 int wharf_export_index(wharf_handle* h, uint64_t* counts, uint64_t* keys, uint32_t* nexts);
 
+/* The same for the vertex window [v0, v1) only: counts[v1 - v0], keys/nexts of
+ * wharf_index_size_range() entries.  Keys stay 64-bit: past n*wpv*L > 2^32
+ * (configs[3]/[4]) the reference's u32 keys (inverted_index.h:14) would wrap.
+ * Lets a caller export a corpus whose whole index does not fit the host. */
+int wharf_index_size_range(wharf_handle* h, uint64_t v0, uint64_t v1, uint64_t* size);
+int wharf_export_index_range(wharf_handle* h, uint64_t v0, uint64_t v1, uint64_t* counts, uint64_t* keys,
+                             uint32_t* nexts);
+
 /* The walks in the reference's pairing-encoded CompressedWalks form
  * (walks/compressed_walks.h:49-66, pairings.h): per vertex, the values
  * Szudzik(wid*L + pos, next) of its stored positions, ascending (the C-tree's

@@ -194,3 +194,49 @@ def test_configs1_full_size_node2vec_generation(W, torch):
     mine = w[:, w0:w0 + 4096].T.contiguous().cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(mine, ref.walks_range(w0, w0 + 4096))
     g.destroy()
+
+
+def test_index_keys_past_2_32(W, torch):
+    """n * wpv * L > 2^32 stored positions (configs[3]/[4]'s regime, where the
+    reference's u32 keys wid*L+pos wrap, inverted_index.h:14): n = 2^20, wpv 255
+    (the u8 maximum), L = 17 -> 4.46 G positions.  The index of a vertex window
+    (wharf_export_index_range) is checked entry for entry against the walk
+    matrix on the device: exactly the window's occurrences, keys ascending per
+    vertex, 64-bit keys above 2^32 present and equal to wid*L + pos of a walk
+    that holds the vertex there, next = the following position."""
+    n, wpv, Lk = 1 << 20, 255, 17
+    cfg = W.WharfConfig(walks_per_vertex=wpv, walk_length=Lk, deterministic=False, seed=11)
+    g = W.WharfMH.from_rmat(n, 8_000_000, 2 * n, seed=4, config=cfg)
+    g.generate_initial_random_walks()
+    Wn = g.number_of_walks
+    assert n * wpv * Lk > (1 << 32) and Wn == n * wpv
+    t = torch.empty((Lk, Wn), dtype=torch.int32, device="cuda:0")
+    g.export_walks_device(t.data_ptr(), layout="position")
+    torch.cuda.synchronize()
+    tv = t.view(torch.int32)
+    for v0, v1 in ((0, 3), (n // 2, n // 2 + 64), (n - 40, n)):
+        counts, keys, nexts = g.inverted_index(v0, v1)
+        assert len(counts) == v1 - v0 and int(counts.sum()) == len(keys)
+        # expected entries from the matrix: positions holding a window vertex
+        # (one position row at a time: torch.nonzero over > 2^32 elements overflows)
+        ps, lis = [], []
+        for p in range(Lk):
+            row = tv[p]
+            li = torch.nonzero((row >= v0) & (row < v1)).flatten()
+            lis.append(li)
+            ps.append(torch.full_like(li, p))
+        pos, li = torch.cat(ps), torch.cat(lis)
+        v = tv[pos, li].long()
+        key = li * Lk + pos                     # full-graph handle: local column li = r * n + v = wid
+        nxt = torch.where(pos + 1 < Lk, tv[(pos + 1).clamp(max=Lk - 1), li], torch.full_like(pos, -2, dtype=torch.int32))
+        order = torch.argsort((v - v0) * (1 << 40) + key)
+        exp_keys = key[order].cpu().numpy().astype(np.uint64)
+        exp_next = nxt[order].cpu().numpy().astype(np.int64).astype(np.uint32)
+        exp_counts = torch.bincount(v - v0, minlength=v1 - v0).cpu().numpy()
+        np.testing.assert_array_equal(counts, exp_counts)
+        np.testing.assert_array_equal(keys, exp_keys)
+        np.testing.assert_array_equal(nexts, exp_next)
+        if v0 == n - 40:
+            assert int(keys.max()) >= (1 << 32)      # ids of the last rounds: keys past u32
+        del ps, lis, pos, li, v, key, nxt, order
+    g.destroy()
