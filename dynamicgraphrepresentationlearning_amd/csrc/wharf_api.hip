@@ -274,11 +274,16 @@ struct wharf_handle {
 
     void read_counters()
     {
-        unsigned long long c[2];
-        HIPCHK(hipMemcpyAsync(c, counters.p, 16, hipMemcpyDeviceToHost, s));
+        unsigned long long c[7] = {};
+        HIPCHK(hipMemcpyAsync(c, counters.p, 56, hipMemcpyDeviceToHost, s));
         sync();
         st.steps = c[0];
         st.accepts = c[1];
+#ifdef WHARF_INIT_STATS
+        fprintf(stderr, "[init-stats] epoch %u: steps %llu inits %llu distinct %llu deferred %llu sweep-lane-slots %llu "
+                        "list-lane-slots %llu\n", epoch, c[0], c[3], c[4], c[2], c[5], c[6]);
+        HIPCHK(hipMemsetAsync(counters.as<unsigned long long>() + 3, 0, 32, s));
+#endif
     }
 };
 
@@ -395,18 +400,6 @@ void rmat_keys(wharf_handle* h, uint64_t edges_number, uint64_t vertices_number,
     h->k1.ensure(std::max<uint64_t>(total, 1) * 8);
     h->k2.ensure(std::max<uint64_t>(total, 1) * 8);
     launch_rmat_keys(p, edges_number, directed, h->k1.as<uint64_t>(), h->s);
-}
-
-// node2vec MH: affected walks a wave needs to re-walk them in place
-// (lock-step sweep, full-row stores); sparser waves defer theirs to the
-// compacted list kernel.  WHARF_LOCKSTEP_MIN: 0 = never defer, 65 = always.
-// (DeepWalk / deterministic steps are cheap enough that the sweep wins at
-// every density measured: configs[3] with 32 % of walks affected, 233 ms
-// swept vs 372 ms deferred.)
-uint32_t lockstep_min()
-{
-    const char* e = getenv("WHARF_LOCKSTEP_MIN");
-    return e ? (uint32_t)std::max(0, atoi(e)) : 40u;
 }
 
 int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, uint32_t flags,
@@ -576,7 +569,6 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             HIPCHK(hipMemsetAsync(h->counters.p, 0, 24, s));
             WalkArgs a = h->walk_args();
             a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
-            a.lockstep_min = lockstep_min();
             // deterministic mode: suffixes walked once per (round, batch source) and copied
             // (k_det_suffix + k_rewalk_chunked<true>) while the table stays small; WHARF_NO_MEMO=1 (tests)
             // re-walks every suffix (k_rewalk_sweep)
@@ -595,7 +587,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
                 a.memo_k = k;
                 a.memo_stride = (uint32_t)stride4;
             }
-            if (!a.scan_only && a.lockstep_min > 0 && a.model == kNode2Vec && !a.det) {   // k_rewalk_list
+            if (a.model == kNode2Vec && !a.det) {   // k_rewalk_plan's compacted, sorted re-walk list
                 h->defer.ensure(h->W * 8);
                 a.defer = h->defer.as<uint64_t>();
             }

@@ -42,8 +42,7 @@ struct WalkArgs {
     float inv_p, inv_q;
     int model, init, det;
     int scan_only;               // re-walk: only find rewalk points (apply_walk_updates=false)
-    uint64_t* defer;             // re-walk: walks of sparse waves, {li | p << 56}, count in counters[2]
-    uint32_t lockstep_min;       // re-walk: a wave with fewer affected walks defers them to `defer`
+    uint64_t* defer;             // node2vec re-walk list {li | p << 56}, tickets << 40 | count in counters[2]
     // deterministic re-walk by suffix table (k_det_suffix + k_rewalk_chunked<true>), or memo == null
     uint32_t* memo;              // [wpv][k][memo_stride]: walk from batch source i in round r, new graph
     const uint32_t* src_idx;     // [n]: index of a batch source in the run table (read for sources only)

@@ -11,6 +11,7 @@
 //   ehash          node2vec: edge set for has_edge (32-B buckets)
 //   bitmap[n/32]   batch-source set for the rewalk-point scan, + its Bloom filter
 #include <cstdlib>
+#include <string>
 
 #include "wharf_kernels.h"
 
@@ -308,6 +309,18 @@ __device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc,
     } else if (need) {
         an = anchor_init(a, rc, rp, cls);
     }
+#ifdef WHARF_INIT_STATS
+    // A/B probe: inits vs distinct states initialised (the first writer's CAS
+    // from the stale entry succeeds; a duplicate finds the value already there)
+    if (need && ein >= 0) {
+        const uint64_t nv = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+        unsigned long long* slot = reinterpret_cast<unsigned long long*>(a.anchor + (uint64_t)ein * kAnchorStride);
+        const bool won = atomicCAS(slot, (unsigned long long)anc, (unsigned long long)nv) == (unsigned long long)anc;
+        atomicAdd(a.counters + 3, 1ull);
+        if (won) atomicAdd(a.counters + 4, 1ull);
+    }
+    return an;
+#endif
     if (need && ein >= 0) a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     return an;
 }
@@ -744,96 +757,141 @@ void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStr
     if (k) hipLaunchKernelGGL(k_src_index, grid_for(k, 256), 256, 0, s, runs, k, src_idx);
 }
 
-// Fused rewalk-point scan + suffix re-walk, node2vec MH.  Setting up a
-// node2vec walker is a chain of dependent loads (rows of cur and prev, the
-// binary search for the anchor-cache slot of the edge prev -> cur), which
-// would stall the interleaved sweep once per distinct rewalk point of the
-// wave.  Three phases per wave instead:
-//   A. each lane scans its old walk (coalesced row reads, bitmap test) up to
-//      its rewalk point or the walk's end;
-//   B. every affected lane builds its walker state (rows of cur / prev, the
-//      node2vec anchor-cache slot) — one dependent chain for the whole wave;
-//   C. the wave sweeps positions from its smallest rewalk point in lock step:
-//      walking lanes write new vertices, the others re-write the old value
-//      they read, so every row of a wave is one full 256-B store.  Rewalk
-//      points differ from lane to lane; a lane-at-its-own-pace loop would make
-//      each store instruction hit up to 64 rows with 4-B partial-line writes
-//      (measured 1.4x slower on configs[2]).
-template <int MODEL, bool DET>
-__global__ __launch_bounds__(256) void k_rewalk(WalkArgs a)
+// node2vec MH re-walk, two kernels.  Setting up a node2vec walker is a chain
+// of dependent loads (rows of cur and prev, the binary search for the
+// anchor-cache slot of prev -> cur) and its steps carry wave-cooperative
+// anchor inits, so the re-walk is bound by dependent-gather latency times the
+// lanes that have work: idle lanes are lost throughput.
+//
+// k_rewalk_plan: per block of 256 walks, the rewalk-point scan (coalesced row
+// reads, Bloom filter in LDS + bitmap), then a counting sort of the block's
+// re-walking walks by rewalk point in LDS, appended to one compacted list
+// {li | p << 56} (a packed atomic hands each block its offset and a ticket;
+// odd tickets store their run descending, so two blocks that meet inside a
+// wave meet at similar rewalk points).
+//
+// k_rewalk_sorted: each wave takes 64 consecutive list entries — walks of one
+// block (their stores share the block's 1 KB row segments in L2) at nearly the
+// same rewalk point — and sweeps positions in lock step from the smallest.
+// Replaces a fused per-wave sweep over the walk matrix (each wave swept 64
+// consecutive walks from their smallest rewalk point: ~58 % of lane-steps
+// idle on configs[2], and sparse waves had to be deferred to the flattened
+// list kernel): configs[2] node2vec batch 73.7 -> 63.6 ms, configs[4]-shaped
+// (scale 24, wpv 1) re-walk 51.7 / 43.9 -> 39.1 / 31.5 ms; the flattened
+// kernel over the same sorted list: 104 ms / 47.9 ms (scattered stores).
+constexpr uint64_t kListMask = (1ull << 40) - 1;   // counters[2]: tickets << 40 | list entries
+
+__global__ __launch_bounds__(256) void k_rewalk_plan(WalkArgs a)
 {
     __shared__ uint32_t s_bloom[kBloomWords];
+    __shared__ uint32_t s_bin[256];                        // count, then cursor, per rewalk point (255: none)
+    __shared__ uint32_t s_wsum[kWavesPerBlock];
+    __shared__ unsigned long long s_ticket;
     bloom_to_lds(a, s_bloom);
-    uint32_t steps = 0, accepts = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    if (blockDim.x != 256) __builtin_trap();               // one histogram bin per thread
     uint32_t* __restrict__ walks = a.walks;
     const uint64_t W = a.W;
-    const uint32_t L = a.L;
-    for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += stride) {
-        const uint64_t r = li / a.n_loc;
-        const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
-        const uint64_t wid = r * a.n + v;
-        const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
-        const uint64_t* __restrict__ rt = DET ? a.rtab + r * L : nullptr;
-        // A. scan
-        uint32_t p = kNoRewalk, x = v, xprev = v;
-        uint32_t xn = L > 1 ? walks[W + li] : kSent;   // next position, prefetched
-        for (uint32_t pos = 0; pos < L; pos++) {
-            if (pos > 0) {
-                xprev = x;
-                x = xn;
-                if (x == kSent) break;
-                if (pos + 1 < L) xn = walks[(uint64_t)(pos + 1) * W + li];
+    const uint32_t L = a.L, t = threadIdx.x, lane = __lane_id();
+    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < W; base += (uint64_t)gridDim.x * 256) {
+        const uint64_t li = base + t;
+        uint32_t p = kNoRewalk;
+        if (li < W) {
+            const uint64_t r = li / a.n_loc;
+            uint32_t x = (uint32_t)(a.lo + (li - r * a.n_loc));
+            uint32_t xn = L > 1 ? walks[W + li] : kSent;   // next position, prefetched
+            for (uint32_t pos = 0; pos < L; pos++) {
+                if (pos > 0) {
+                    x = xn;
+                    if (x == kSent) break;
+                    if (pos + 1 < L) xn = walks[(uint64_t)(pos + 1) * W + li];
+                }
+                if (is_source(a, s_bloom, x)) { p = pos; break; }
             }
-            if (is_source(a, s_bloom, x)) { p = pos; break; }
+            a.aff[li] = (uint8_t)p;
         }
-        a.aff[li] = (uint8_t)p;
         if (a.scan_only) continue;
-        const bool active = p + 1 < L;   // affected, and something after the rewalk point
-        if (a.defer) {
-            // A wave with few affected walks would sweep with most lanes idle:
-            // hand its walks to k_rewalk_list (one atomic per wave) instead.
-            const uint64_t mask = __ballot(active);
-            const uint32_t cnt = (uint32_t)__popcll(mask);
-            if (cnt == 0) continue;
-            if (cnt < a.lockstep_min) {
-                const uint32_t lane = __lane_id(), leader = (uint32_t)__ffsll((long long)mask) - 1;
-                unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(a.counters + 2, (unsigned long long)cnt);
-                base = __shfl(base, (int)leader, 64);
-                if (active) a.defer[base + __popcll(mask & ((1ull << lane) - 1))] = li | ((uint64_t)p << 56);
-                continue;
-            }
+        const uint32_t key = (li < W && p + 1 < L) ? p : 255u;   // re-walking: something after the point
+        s_bin[t] = 0;
+        __syncthreads();
+        atomicAdd(&s_bin[key], 1u);
+        __syncthreads();
+        const uint32_t c = s_bin[t];
+        uint32_t incl = c;                                 // exclusive scan of the 256 bins
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+            if ((int)lane >= o) incl += y;
         }
-        // B. walker state at the rewalk point
+        if (lane == 63) s_wsum[t >> 6] = incl;
+        __syncthreads();
+        uint32_t before = 0;
+        for (uint32_t w = 0; w < (t >> 6); w++) before += s_wsum[w];
+        s_bin[t] = before + incl - c;
+        __syncthreads();
+        const uint32_t nact = s_bin[255];                  // entries ranked before the "none" bin
+        if (t == 0) s_ticket = nact ? atomicAdd(a.counters + 2, (1ull << 40) | nact) : 0ull;
+        __syncthreads();
+        if (key != 255u) {
+            const uint32_t rank = atomicAdd(&s_bin[key], 1u);
+            const uint64_t tk = s_ticket;
+            const uint32_t at = ((tk >> 40) & 1u) ? nact - 1 - rank : rank;
+            a.defer[(tk & kListMask) + at] = li | ((uint64_t)p << 56);
+        }
+        __syncthreads();                                   // s_bin / s_ticket are reused
+    }
+}
+
+// (105 VGPRs, 4 waves/SIMD; forcing 5 spills 12 B and measured no faster:
+// configs[2] node2vec batch 65.4 vs 63.6 ms)
+template <int MODEL, bool DET>
+__global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
+{
+    uint32_t steps = 0, accepts = 0;
+    uint32_t* __restrict__ walks = a.walks;
+    const uint64_t W = a.W, cnt = a.counters[2] & kListMask;
+    const uint32_t L = a.L, ep = a.epoch << 4;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t c0 = wave * 64; c0 < cnt; c0 += nwaves * 64) {
+        const uint64_t e = c0 + __lane_id();
+        const bool active = e < cnt;
+        uint64_t li = 0;
+        uint32_t p = L, wlo = 0, whi = 0;
+        const uint64_t* __restrict__ rt = nullptr;
         Walker w;
         w.rc.deg = 0;
-        if (active) walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, w);
-        // C. lock-step sweep from the wave's smallest rewalk point
+        if (active) {
+            const uint64_t ent = a.defer[e];
+            li = ent & ((1ull << 56) - 1);
+            p = (uint32_t)(ent >> 56);
+            const uint64_t r = li / a.n_loc;
+            const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
+            wlo = (uint32_t)wid;
+            whi = (uint32_t)(wid >> 32);
+            if constexpr (DET) rt = a.rtab + r * L;
+            const uint32_t x = walks[(uint64_t)p * W + li];
+            const uint32_t xprev = p ? walks[(uint64_t)(p - 1) * W + li] : x;
+            walk_state<MODEL, DET>(a, x, xprev, p, wlo, whi, ep, w);
+        }
         uint32_t first = active ? p + 1 : L;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, o, 64));
         for (uint32_t pos = first; pos < L; pos++) {
-            const uint64_t at = (uint64_t)pos * W + li;
-            uint32_t val;
-            if (active && pos > p) {
-                val = kSent;
-                if (w.rc.deg) {
-                    val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts);
-                    steps++;
-                }
-            } else {
-                val = walks[at];   // not (yet) re-walking: keep the old value
+            if (!(active && pos > p)) continue;
+            uint32_t val = kSent;
+            if (w.rc.deg) {
+                val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts);
+                steps++;
             }
-            walks[at] = val;
+            walks[(uint64_t)pos * W + li] = val;
         }
     }
     wave_add(a.counters + 0, steps);
     wave_add(a.counters + 1, accepts);
 }
 
-// Re-walk of the deferred walks (sparse waves of k_rewalk): a compacted list,
-// lanes at their own pace.  One flattened loop — a lane whose walk is done
+// Flattened alternative to k_rewalk_sorted over the same list
+// (WHARF_N2V_REWALK=flat): lanes at their own pace.  One flattened loop — a lane whose walk is done
 // takes its next list entry in the same iteration instead of waiting for the
 // rest of its wave.  Stores land in scattered rows (partial lines), the price
 // of keeping every lane busy; results are identical to the lock-step sweep
@@ -842,7 +900,7 @@ template <int MODEL, bool DET>
 __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
 {
     uint32_t steps = 0, accepts = 0;
-    const uint64_t cnt = a.counters[2];
+    const uint64_t cnt = a.counters[2] & kListMask;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t* __restrict__ walks = a.walks;
     const uint64_t W = a.W;
@@ -870,6 +928,9 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
             pos = p + 1;
         }
         if (!__any(pos < L)) break;
+#ifdef WHARF_INIT_STATS
+        if (__lane_id() == 0) atomicAdd(a.counters + 6, 64ull);
+#endif
         if (pos < L) {
             uint32_t val = kSent;
             if (w.rc.deg) {
@@ -910,8 +971,15 @@ static unsigned walk_grid(uint64_t W)
     return (unsigned)std::min<uint64_t>(full, (uint64_t)cu_count() * per_cu);
 }
 
-// resident lanes for the deferred-walk list kernel (8 blocks of 256 per CU)
+// resident lanes for the node2vec re-walk list kernels (8 blocks of 256 per CU)
 static unsigned list_grid() { return cu_count() * 8; }
+
+// WHARF_N2V_REWALK=flat: the flattened list kernel instead of the sorted lock-step one (A/B, tests)
+static bool flat_list()
+{
+    const char* e = getenv("WHARF_N2V_REWALK");
+    return e && std::string(e) == "flat";
+}
 
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
 {
@@ -924,8 +992,11 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
 #define WHARF_LAUNCH(M, D)                                                                   \
     do {                                                                                     \
         if (rewalk && M == kNode2Vec) {                                                      \
-            hipLaunchKernelGGL((k_rewalk<M, D>), grid, block, 0, s, a);                      \
-            if (a.defer && !a.scan_only) hipLaunchKernelGGL((k_rewalk_list<M, D>), lgrid, block, 0, s, a); \
+            hipLaunchKernelGGL(k_rewalk_plan, grid, block, 0, s, a);                         \
+            if (!a.scan_only) {                                                              \
+                if (flat_list()) hipLaunchKernelGGL((k_rewalk_list<M, D>), lgrid, block, 0, s, a); \
+                else hipLaunchKernelGGL((k_rewalk_sorted<M, D>), lgrid, block, 0, s, a);     \
+            }                                                                                \
         } else if (rewalk) {                                                                 \
             hipLaunchKernelGGL((k_rewalk_sweep<M, D>), grid, block, 0, s, a);                \
         } else {                                                                             \

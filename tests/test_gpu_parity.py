@@ -307,10 +307,10 @@ def test_affected_ids_on_device_match_host_list(W):
     gd.destroy()
 
 
-# (WHARF_LOCKSTEP_MIN, WHARF_MOVE_NO_LDS, WHARF_FORCE_RECORD_REBUILD, neighbour filter, WHARF_NO_MEMO,
+# (WHARF_N2V_REWALK, WHARF_MOVE_NO_LDS, WHARF_FORCE_RECORD_REBUILD, neighbour filter, WHARF_NO_MEMO,
 #  WHARF_NO_CHUNKED_SCAN)
-PATHS = {"sweep/patch-lds": ("0", "0", "0", "on", "1", "0"), "deferred/inplace-l2": ("65", "1", "1", "noslack", "0", "0"),
-         "mixed/inplace-lds": ("40", "0", "1", "off", "0", "1"), "mixed/gather": ("16", "1", "2", "on", "1", "1")}
+PATHS = {"sorted/patch-lds": ("sorted", "0", "0", "on", "1", "0"), "flat/inplace-l2": ("flat", "1", "1", "noslack", "0", "0"),
+         "sorted/inplace-lds": ("sorted", "0", "1", "off", "0", "1"), "flat/gather": ("flat", "1", "2", "on", "1", "1")}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -318,9 +318,9 @@ PATHS = {"sweep/patch-lds": ("0", "0", "0", "on", "1", "0"), "deferred/inplace-l
 def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     """Every re-walk kernel and every CSR-update path reproduces the oracle's
     corpus, counters, affected ids and CSR.  Re-walk: the interleaved sweep
-    (DeepWalk, deterministic); for node2vec the phased sweep
-    (WHARF_LOCKSTEP_MIN=0), the compacted deferred list (=65: every wave
-    defers) and a mix.  CSR update: the record patch with the source table in
+    (DeepWalk, deterministic); for node2vec the planned, sorted re-walk list
+    swept in lock step (k_rewalk_sorted) or by lanes at their own pace
+    (WHARF_N2V_REWALK=flat, k_rewalk_list).  CSR update: the record patch with the source table in
     LDS or the bucketed L2 table (WHARF_MOVE_NO_LDS), into a second record
     buffer, in place (chunked), or records rebuilt by a gather with node2vec
     anchors kept aside (WHARF_FORCE_RECORD_REBUILD=1 / 2).  node2vec anchor
@@ -330,12 +330,12 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     copy) and by walking every suffix (WHARF_NO_MEMO=1, k_rewalk_sweep).
     Rewalk points alone (apply_walk_updates = false): the chunked scan, or
     with WHARF_NO_CHUNKED_SCAN=1 the sweep kernels in scan-only mode."""
-    lockstep_min, no_lds, force, filt, no_memo, no_chunked = PATHS[path]
+    n2v_list, no_lds, force, filt, no_memo, no_chunked = PATHS[path]
     monkeypatch.setenv("WHARF_NO_MEMO", no_memo)
     monkeypatch.setenv("WHARF_NO_CHUNKED_SCAN", no_chunked)
     monkeypatch.setenv("WHARF_NO_NEIGHBOUR_FILTER", "1" if filt == "off" else "0")
     monkeypatch.setenv("WHARF_FILTER_NO_SLACK", "1" if filt == "noslack" else "0")
-    monkeypatch.setenv("WHARF_LOCKSTEP_MIN", lockstep_min)
+    monkeypatch.setenv("WHARF_N2V_REWALK", n2v_list)
     monkeypatch.setenv("WHARF_MOVE_NO_LDS", no_lds)
     monkeypatch.setenv("WHARF_FORCE_RECORD_REBUILD", force)
     base = O.generate_batch_of_edges(50000, 1 << 13, 6, False, False)
