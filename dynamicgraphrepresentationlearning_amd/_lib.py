@@ -84,6 +84,7 @@ SIGNATURES = {
     "wharf_generate": (_I, [_P]),
     "wharf_insert_edges": (_I, [_P, _U64, _P, _U32, _P, _P]),
     "wharf_delete_edges": (_I, [_P, _U64, _P, _U32, _P, _P]),
+    "wharf_batch_walk_update": (_I, [_P, _P, _U64, _U32, _P, _P]),
     "wharf_number_of_vertices": (_I, [_P, _P]),
     "wharf_number_of_edges": (_I, [_P, _P]),
     "wharf_shard": (_I, [_P, _P, _P, _P]),

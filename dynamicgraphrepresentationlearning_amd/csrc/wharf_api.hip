@@ -1,6 +1,7 @@
 // C ABI of the WharfMH walk engine (include/wharf_gpu.h): handle management,
 // the graph / batch pipelines (rocPRIM sorts, selects and scans on the
 // handle's stream) and the host side of every entry point.
+#include <algorithm>
 #include <cstring>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -402,6 +403,75 @@ void rmat_keys(wharf_handle* h, uint64_t edges_number, uint64_t vertices_number,
     launch_rmat_keys(p, edges_number, directed, h->k1.as<uint64_t>(), h->s);
 }
 
+// Rewalk points + suffix re-walk (wharfmh.h:519-537, batch_walk_update
+// 733-923) of every owned walk that holds a vertex of the bitmap; h->runs
+// holds the k sources (the deterministic suffix table is keyed by them), and
+// ev[1] marks the start of the walk update.
+void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected_out, uint64_t* n_affected)
+{
+    hipStream_t s = h->s;
+    if (h->has_walks && h->W) {
+        HIPCHK(hipMemsetAsync(h->counters.p, 0, 24, s));
+        WalkArgs a = h->walk_args();
+        a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
+        // deterministic mode: suffixes walked once per (round, batch source) and copied
+        // (k_det_suffix + k_rewalk_chunked<true>) while the table stays small; WHARF_NO_MEMO=1 (tests)
+        // re-walks every suffix (k_rewalk_sweep)
+        const uint64_t stride4 = (h->L + 3) & ~3ull;
+        const char* no_memo = getenv("WHARF_NO_MEMO");
+        if (a.det && !a.scan_only && k && !(no_memo && atoi(no_memo)) &&
+            (uint64_t)h->wpv * k * stride4 * 4 <= (256ull << 20)) {
+            h->srcidx.ensure(std::max<uint64_t>(h->n, 1) * 4);
+            // kMemoPad words before and after the table: k_rewalk_chunked reads whole
+            // chunks around a row (values outside the row are never written)
+            h->memo.ensure(((uint64_t)h->wpv * k * stride4 + 2 * kMemoPad) * 4);
+            launch_src_index(h->runs.as<RunInfo>(), k, h->srcidx.as<uint32_t>(), s);
+            a.memo = h->memo.as<uint32_t>() + kMemoPad;
+            a.src_idx = h->srcidx.as<uint32_t>();
+            a.runs = h->runs.as<RunInfo>();
+            a.memo_k = k;
+            a.memo_stride = (uint32_t)stride4;
+        }
+        if (a.model == kNode2Vec && !a.det) {   // k_rewalk_plan's compacted, sorted re-walk list
+            h->defer.ensure(h->W * 8);
+            a.defer = h->defer.as<uint64_t>();
+        }
+        HIPCHK(hipEventRecord(h->ev[2], s));
+        launch_walk(a, true, s);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(h->ev[3], s));
+        // ascending affected walk ids: count per block, scan, write
+        const unsigned nb = aff_blocks(h->W);
+        h->sel.ensure((uint64_t)(nb + 1) * 8);
+        uint32_t* bcount = h->sel.as<uint32_t>();
+        uint32_t* boff = bcount + nb + 1;
+        HIPCHK(hipMemsetAsync(bcount + nb, 0, 4, s));
+        launch_aff_count(h->aff.as<uint8_t>(), h->W, bcount, s);
+        h->rp([&](void* t, size_t& b) {
+            return rocprim::exclusive_scan(t, b, bcount, boff, 0u, (size_t)nb + 1, rocprim::plus<uint32_t>(), s);
+        });
+        const bool on_device = affected_out && (flags & WHARF_AFFECTED_DEVICE);
+        if (!on_device) h->pairs.ensure(h->W * 4);
+        launch_aff_write(h->aff.as<uint8_t>(), h->W, boff, h->n, h->n_loc, h->lo,
+                         on_device ? affected_out : h->pairs.as<uint32_t>(), s);
+        uint32_t naff32 = 0;
+        HIPCHK(hipMemcpyAsync(&naff32, boff + nb, 4, hipMemcpyDeviceToHost, s));
+        h->sync();
+        const uint64_t naff = naff32;
+        if (affected_out && !on_device && naff) {
+            HIPCHK(hipMemcpyAsync(affected_out, h->pairs.p, naff * 4, hipMemcpyDeviceToHost, s));
+            h->sync();
+        }
+        h->st.affected = naff;
+        if (n_affected) *n_affected = naff;
+        h->read_counters();
+        h->st.last_walk_kernel_ms = h->elapsed(2, 3);
+        h->st.last_walk_update_ms = h->elapsed(1, 3);
+    } else {
+        h->sync();
+    }
+}
+
 int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, uint32_t flags,
               uint32_t* affected_out, uint64_t* n_affected)
 {
@@ -565,66 +635,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
 
         // 5. rewalk points + suffix re-walk in one pass over the walk matrix
         //    (wharfmh.h:519-537 and batch_walk_update 733-923)
-        if (h->has_walks && h->W) {
-            HIPCHK(hipMemsetAsync(h->counters.p, 0, 24, s));
-            WalkArgs a = h->walk_args();
-            a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
-            // deterministic mode: suffixes walked once per (round, batch source) and copied
-            // (k_det_suffix + k_rewalk_chunked<true>) while the table stays small; WHARF_NO_MEMO=1 (tests)
-            // re-walks every suffix (k_rewalk_sweep)
-            const uint64_t stride4 = (h->L + 3) & ~3ull;
-            const char* no_memo = getenv("WHARF_NO_MEMO");
-            if (a.det && !a.scan_only && k && !(no_memo && atoi(no_memo)) &&
-                (uint64_t)h->wpv * k * stride4 * 4 <= (256ull << 20)) {
-                h->srcidx.ensure(std::max<uint64_t>(h->n, 1) * 4);
-                // kMemoPad words before and after the table: k_rewalk_chunked reads whole
-                // chunks around a row (values outside the row are never written)
-                h->memo.ensure(((uint64_t)h->wpv * k * stride4 + 2 * kMemoPad) * 4);
-                launch_src_index(h->runs.as<RunInfo>(), k, h->srcidx.as<uint32_t>(), s);
-                a.memo = h->memo.as<uint32_t>() + kMemoPad;
-                a.src_idx = h->srcidx.as<uint32_t>();
-                a.runs = h->runs.as<RunInfo>();
-                a.memo_k = k;
-                a.memo_stride = (uint32_t)stride4;
-            }
-            if (a.model == kNode2Vec && !a.det) {   // k_rewalk_plan's compacted, sorted re-walk list
-                h->defer.ensure(h->W * 8);
-                a.defer = h->defer.as<uint64_t>();
-            }
-            HIPCHK(hipEventRecord(h->ev[2], s));
-            launch_walk(a, true, s);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(h->ev[3], s));
-            // ascending affected walk ids: count per block, scan, write
-            const unsigned nb = aff_blocks(h->W);
-            h->sel.ensure((uint64_t)(nb + 1) * 8);
-            uint32_t* bcount = h->sel.as<uint32_t>();
-            uint32_t* boff = bcount + nb + 1;
-            HIPCHK(hipMemsetAsync(bcount + nb, 0, 4, s));
-            launch_aff_count(h->aff.as<uint8_t>(), h->W, bcount, s);
-            h->rp([&](void* t, size_t& b) {
-                return rocprim::exclusive_scan(t, b, bcount, boff, 0u, (size_t)nb + 1, rocprim::plus<uint32_t>(), s);
-            });
-            const bool on_device = affected_out && (flags & WHARF_AFFECTED_DEVICE);
-            if (!on_device) h->pairs.ensure(h->W * 4);
-            launch_aff_write(h->aff.as<uint8_t>(), h->W, boff, h->n, h->n_loc, h->lo,
-                             on_device ? affected_out : h->pairs.as<uint32_t>(), s);
-            uint32_t naff32 = 0;
-            HIPCHK(hipMemcpyAsync(&naff32, boff + nb, 4, hipMemcpyDeviceToHost, s));
-            h->sync();
-            const uint64_t naff = naff32;
-            if (affected_out && !on_device && naff) {
-                HIPCHK(hipMemcpyAsync(affected_out, h->pairs.p, naff * 4, hipMemcpyDeviceToHost, s));
-                h->sync();
-            }
-            h->st.affected = naff;
-            if (n_affected) *n_affected = naff;
-            h->read_counters();
-            h->st.last_walk_kernel_ms = h->elapsed(2, 3);
-            h->st.last_walk_update_ms = h->elapsed(1, 3);
-        } else {
-            h->sync();
-        }
+        walk_update(h, k, flags, affected_out, n_affected);
         h->st.last_graph_update_ms = h->elapsed(0, 1);
         h->st.last_csr_move_ms = h->elapsed(4, 5);
         h->st.last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -774,6 +785,41 @@ int wharf_delete_edges(wharf_handle* h, uint64_t m, const uint32_t* pairs, uint3
                        uint64_t* n_affected)
 {
     return do_update(h, false, m, pairs, flags, affected_out, n_affected);
+}
+
+int wharf_batch_walk_update(wharf_handle* h, const uint32_t* sources, uint64_t k, uint32_t flags,
+                            uint32_t* affected_out, uint64_t* n_affected)
+{
+    return guarded(h, [&] {
+        REQUIRE(h, WHARF_E_INVALID, "null handle");
+        REQUIRE(k == 0 || sources, WHARF_E_INVALID, "sources is null");
+        auto t0 = std::chrono::steady_clock::now();
+        h->st.affected = 0;
+        h->st.steps = h->st.accepts = 0;
+        h->st.batch_edges = 0;
+        h->st.last_graph_update_ms = h->st.last_walk_update_ms = h->st.last_walk_kernel_ms = 0;
+        h->st.last_csr_move_ms = 0;
+        h->st.last_moved_slots = 0;
+        if (n_affected) *n_affected = 0;
+        // the vertex set of the MapOfChanges: sorted, deduplicated, validated
+        std::vector<uint32_t> src(sources, sources + k);
+        std::sort(src.begin(), src.end());
+        src.erase(std::unique(src.begin(), src.end()), src.end());
+        REQUIRE(src.empty() || src.back() < h->n, WHARF_E_INVALID, "source vertex >= number_of_vertices()");
+        k = src.size();
+        hipStream_t s = h->s;
+        HIPCHK(hipMemsetAsync(h->bitmap.p, 0, (h->bitmap_words() + kBloomWords) * 4, s));
+        if (k) {
+            h->k1.ensure(k * 4);
+            HIPCHK(hipMemcpyAsync(h->k1.p, src.data(), k * 4, hipMemcpyHostToDevice, s));
+            h->runs.ensure(k * sizeof(RunInfo));
+            launch_mark_sources(h->k1.as<uint32_t>(), k, h->runs.as<RunInfo>(), h->bitmap.as<uint32_t>(),
+                                h->bitmap.as<uint32_t>() + h->bitmap_words(), s);
+        }
+        HIPCHK(hipEventRecord(h->ev[1], s));
+        walk_update(h, k, flags | WHARF_APPLY_WALK_UPDATES, affected_out, n_affected);
+        h->st.last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    });
 }
 
 int wharf_number_of_vertices(const wharf_handle* h, uint64_t* n)

@@ -95,6 +95,8 @@ void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
                      RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, uint32_t* row_epoch, uint32_t epoch,
                      hipStream_t s);
+void launch_mark_sources(const uint32_t* src, uint64_t k, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom,
+                         hipStream_t s);
 void launch_run_tables(const RunInfo* runs, uint64_t k, const uint32_t* cf, uint64_t mb, uint64_t n, uint64_t m,
                        uint32_t* tabs, RunIndex* x, hipStream_t s);
 void launch_new_offsets(const uint64_t* off, uint64_t n, const RunIndex& x, const uint32_t* cf, uint64_t mb, int insert,

@@ -1332,6 +1332,23 @@ __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* _
     }
 }
 
+// batch_walk_update with a caller-given vertex set: the same bitmap, Bloom
+// filter and source table (src only) as k_run_info, no sampler reset
+__global__ void k_mark_sources(const uint32_t* __restrict__ src, uint64_t k, RunInfo* __restrict__ runs,
+                               uint32_t* __restrict__ bitmap, uint32_t* __restrict__ bloom)
+{
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = src[j];
+        RunInfo ri{};
+        ri.src = s;
+        runs[j] = ri;
+        atomicOr(bitmap + (s >> 5), 1u << (s & 31));
+        const uint32_t h = bloom_hash(s), h2 = bloom_hash2(s);
+        atomicOr(bloom + (h >> 5), 1u << (h & 31));
+        atomicOr(bloom + (h2 >> 5), 1u << (h2 & 31));
+    }
+}
+
 // Bucketed index over the source-run table: vtab[b] = {first run with
 // src >= b << vs, the row shift of the vertices of bucket b below it},
 // etab[b] = first run with row offset >= b << es.  A lookup reads one table
@@ -2002,6 +2019,11 @@ void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t 
                      RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, uint32_t* row_epoch, uint32_t epoch,
                      hipStream_t s)
 { hipLaunchKernelGGL(k_run_info, grid_for(k, 256), 256, 0, s, bkeys, run_start, k, mb, off, runs, bitmap, bloom, row_epoch, epoch); }
+
+void launch_mark_sources(const uint32_t* src, uint64_t k, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, hipStream_t s)
+{
+    if (k) hipLaunchKernelGGL(k_mark_sources, grid_for(k, 256), 256, 0, s, src, k, runs, bitmap, bloom);
+}
 void launch_run_tables(const RunInfo* runs, uint64_t k, const uint32_t* cf, uint64_t mb, uint64_t n, uint64_t m,
                        uint32_t* tabs, RunIndex* x, hipStream_t s)
 {

@@ -225,6 +225,21 @@ class WharfMH:
         """wharfmh.h:588."""
         return self._update(L.lib.wharf_delete_edges, edges, sorted, remove_dups, apply_walk_updates, out)
 
+    def batch_walk_update(self, sources, out=None) -> np.ndarray:
+        """wharfmh.h:733: re-walk every walk from its first position holding a
+        vertex of `sources` (the vertex set of the reference's MapOfChanges) on
+        the current graph; returns the affected walk ids (ascending).  After an
+        update with apply_walk_updates=False, passing that batch's sources gives
+        exactly the walks the update would have produced."""
+        src = np.ascontiguousarray(np.asarray(sources, dtype=np.uint32).reshape(-1))
+        buf = out if out is not None else np.empty(max(self.number_of_walks, 1), dtype=np.uint32)
+        if buf.dtype != np.uint32 or len(buf) < self.number_of_walks or not buf.flags.c_contiguous:
+            raise ValueError("out must be a contiguous uint32 array with >= number_of_walks entries")
+        cnt = C.c_uint64()
+        L.check(L.lib.wharf_batch_walk_update(self._h, _ptr(src), len(src), 0, _ptr(buf), C.byref(cnt)), self._h,
+                "batch_walk_update")
+        return buf[: cnt.value]
+
     def walk(self, walk_id: int) -> str:
         """WharfMH::walk (wharfmh.h:365): "v0 v1 ... " with a trailing space."""
         n = C.c_size_t()

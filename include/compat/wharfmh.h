@@ -1,0 +1,370 @@
+// compat/wharfmh.h — source-compatibility layer for driver code written
+// against the reference's <wharfmh.h> (graph/wharfmh.h and what it pulls in:
+// config/config.h, config/globals.h, config/types.h, utils/utility.h and the
+// pbbs / compressed_trees helpers the experiment drivers use).
+//
+// A reference driver (experiments/src/throughput-latency.cpp and the like)
+// compiles unchanged with `-I include/compat -I include` in place of the
+// reference's include dirs, and links libwharf_gpu.so:
+//
+//     g++ -std=c++17 -I include/compat -I include driver.cpp
+//         -L dynamicgraphrepresentationlearning_amd -lwharf_gpu
+//
+// What it provides (each names the reference interface it mirrors):
+//   dygrl::WharfMH            graph/wharfmh.h:21-1105 over the C ABI (include/wharf_gpu.h)
+//   config::*                 config/globals.h:7-29, read when a WharfMH is constructed
+//   types::*                  config/types.h:4-45 (the enums and id types)
+//   graph_update_time_on_*,   config/config.h:10-14: fed with the device time of each
+//   walk_update_time_on_*       update's CSR merge / re-walk (wharf_stats)
+//   utility::generate_batch_of_edges   utils/utility.h:55-146 (device RMAT, bit-exact)
+//   read_unweighted_graph     compressed_trees/common/IO.h:67-106
+//   pbbs::sequence / log2_up / new_array_no_init / free_array, timer, commandLine,
+//   num_workers, default_file_name   the pbbs helpers the drivers touch
+//
+// Semantics that differ from the reference are those of the C ABI (DESIGN.md
+// §4): MH mode draws from counter-based Philox streams keyed by config::seed
+// instead of the time-seeded global config::random, and errors throw
+// wharf::Error instead of calling std::exit.
+#pragma once
+
+#include <sys/time.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <iomanip>
+#include <iostream>
+#include <limits>
+#include <string>
+#include <thread>
+#include <tuple>
+#include <utility>
+#include <vector>
+
+#include "wharfmh.hpp"
+
+// the reference is built with -DEDGELONG (CMakeLists.txt): 64-bit offsets
+using uintV = uint32_t;
+using uintE = uint64_t;
+
+// names the reference's headers make visible unqualified
+using std::cout;
+using std::endl;
+using std::get;
+using std::string;
+using std::tuple;
+
+namespace types {
+using Vertex = uintV;
+using Degree = uintE;
+using WalkID = uint32_t;
+using Position = uint8_t;
+using State = std::pair<Vertex, Vertex>;
+enum RandomWalkModelType { DEEPWALK = WHARF_DEEPWALK, NODE2VEC = WHARF_NODE2VEC };
+enum SamplerInitStartegy { RANDOM = WHARF_INIT_RANDOM, BURNIN = WHARF_INIT_BURNIN, WEIGHT = WHARF_INIT_WEIGHT };
+}  // namespace types
+
+// config/globals.h: same names, types and defaults
+namespace config {
+inline uint8_t walks_per_vertex = 10;
+inline uint8_t walk_length = 80;
+inline types::RandomWalkModelType random_walk_model = types::RandomWalkModelType::NODE2VEC;
+inline float paramP = 4.0f;
+inline float paramQ = 1.0f;
+inline types::SamplerInitStartegy sampler_init_strategy = types::SamplerInitStartegy::WEIGHT;
+inline bool deterministic_mode = true;
+inline uint64_t seed = 0x5EED;   // MH-mode Philox key (the reference: config::random(std::time(nullptr)))
+}  // namespace config
+
+// pbbslib/get_time.h's timer: wall-clock seconds, accumulated between start/stop
+struct timer {
+    double total_time = 0.0, last_time = 0.0;
+    bool on = false;
+    std::string name;
+
+    explicit timer(std::string nm = "PBBS time", bool start_now = true) : name(std::move(nm))
+    {
+        if (start_now) start();
+    }
+    static double now()
+    {
+        timeval tv;
+        gettimeofday(&tv, nullptr);
+        return (double)tv.tv_sec + (double)tv.tv_usec * 1e-6;
+    }
+    void start()
+    {
+        on = true;
+        last_time = now();
+    }
+    double stop()
+    {
+        on = false;
+        const double d = now() - last_time;
+        total_time += d;
+        return d;
+    }
+    void reset()
+    {
+        total_time = 0.0;
+        on = false;
+    }
+    double get_total() const { return on ? total_time + now() - last_time : total_time; }
+    void add(double seconds) { total_time += seconds; }   // device-timed intervals (not in pbbs)
+    void report(double t, const std::string& what) const
+    {
+        const auto f = std::cout.flags();
+        std::cout << name << ": ";
+        if (!what.empty()) std::cout << what << ": ";
+        std::cout << std::fixed << std::setprecision(4) << t << std::endl;
+        std::cout.flags(f);
+    }
+    void reportTotal(const std::string& what) const { report(get_total(), what); }
+    void total()
+    {
+        report(get_total(), "total");
+        total_time = 0.0;
+    }
+};
+
+// config/config.h:10-14
+inline timer graph_update_time_on_insert("GraphUpdateTimeOnInsert", false);
+inline timer walk_update_time_on_insert("WalkUpdateTimeOnInsert", false);
+inline timer graph_update_time_on_delete("GraphUpdateTimeOnDelete", false);
+inline timer walk_update_time_on_delete("WalkUpdateTimeOnDelete", false);
+
+// pbbslib/parse_command_line.h's commandLine: "-opt value" lookups
+struct commandLine {
+    int argc;
+    char** argv;
+    std::string usage;
+
+    commandLine(int c, char** v, std::string u = "bad arguments") : argc(c), argv(v), usage(std::move(u))
+    {
+        if (getOption("-h") || getOption("-help")) badArgument();
+    }
+    [[noreturn]] void badArgument() const
+    {
+        std::cout << "usage: " << argv[0] << " " << usage << std::endl;
+        std::exit(0);
+    }
+    int find(const std::string& opt, bool with_value) const
+    {
+        for (int i = 1; i < argc - (with_value ? 1 : 0); i++)
+            if (opt == argv[i]) return i;
+        return -1;
+    }
+    bool getOption(const std::string& opt) const { return find(opt, false) >= 0; }
+    char* getOptionValue(const std::string& opt) const
+    {
+        const int i = find(opt, true);
+        return i < 0 ? nullptr : argv[i + 1];
+    }
+    std::string getOptionValue(const std::string& opt, const std::string& dflt) const
+    {
+        const int i = find(opt, true);
+        return i < 0 ? dflt : std::string(argv[i + 1]);
+    }
+    long getOptionLongValue(const std::string& opt, long dflt) const
+    {
+        const int i = find(opt, true);
+        if (i < 0) return dflt;
+        const long r = std::atol(argv[i + 1]);
+        if (r < 0) badArgument();
+        return r;
+    }
+    int getOptionIntValue(const std::string& opt, int dflt) const { return (int)getOptionLongValue(opt, dflt); }
+    double getOptionDoubleValue(const std::string& opt, double dflt) const
+    {
+        const int i = find(opt, true);
+        if (i < 0) return dflt;
+        double v = 0;
+        if (std::sscanf(argv[i + 1], "%lf", &v) != 1) badArgument();
+        return v;
+    }
+};
+
+inline const std::string default_file_name = "";
+
+// worker threads of the host scheduler; the walk path itself runs on the GPU
+inline int num_workers()
+{
+    const unsigned h = std::thread::hardware_concurrency();
+    return h ? (int)h : 1;
+}
+
+namespace pbbs {
+template <class T>
+struct sequence : std::vector<T> {
+    using std::vector<T>::vector;
+    sequence() = default;
+    explicit sequence(std::vector<T>&& v) : std::vector<T>(std::move(v)) {}
+    T* to_array()   // hands the elements over as a malloc'd array (free_array releases it)
+    {
+        T* a = (T*)std::malloc(std::max<size_t>(this->size(), 1) * sizeof(T));
+        std::copy(this->begin(), this->end(), a);
+        this->clear();
+        return a;
+    }
+};
+// ceil(log2(i)), 0 for i <= 1
+inline size_t log2_up(size_t i)
+{
+    size_t a = 0;
+    for (size_t b = i > 0 ? i - 1 : 0; b > 0; b >>= 1) a++;
+    return a;
+}
+template <class T> T* new_array_no_init(size_t n) { return (T*)std::malloc(std::max<size_t>(n, 1) * sizeof(T)); }
+template <class T> void free_array(T* a) { std::free((void*)a); }   // USEMALLOC build: pbbs arrays are malloc'd
+}  // namespace pbbs
+
+namespace utility {
+// utils/utility.h:55-146: RMAT edges on graph_size_pow2 = 2^(log2_up(n) - 1)
+// vertices, sorted by (src, dst), duplicates (and self loops unless asked)
+// removed; undirected batches hold both directions.  Generated on GPU 0,
+// bit-exact with the reference; the array is malloc'd (pbbs::free_array).
+inline std::pair<std::tuple<uintV, uintV>*, size_t> generate_batch_of_edges(
+    size_t edges_number, size_t vertices_number, size_t batch_seed, bool self_loops = false, bool directed = true,
+    double a = 0.5, double b = 0.2, double c = 0.1, bool run_seq = false)
+{
+    (void)run_seq;
+    std::vector<uint32_t> pairs(2 * (directed ? edges_number : 2 * edges_number) + 2);
+    uint64_t k = 0;
+    wharf::check(wharf_generate_batch_of_edges(0, edges_number, vertices_number, batch_seed, self_loops, directed, a, b,
+                                               c, pairs.data(), &k),
+                 nullptr, "generate_batch_of_edges");
+    auto* e = pbbs::new_array_no_init<std::tuple<uintV, uintV>>(k);
+    for (uint64_t i = 0; i < k; i++) new (e + i) std::tuple<uintV, uintV>(pairs[2 * i], pairs[2 * i + 1]);
+    return {e, (size_t)k};
+}
+}  // namespace utility
+
+// compressed_trees/common/IO.h:67-106: a Ligra AdjacencyGraph file -> (n, m,
+// offsets[n], edges[m]), malloc'd (WharfMH takes them over with free_memory)
+inline std::tuple<size_t, size_t, uintE*, uintV*> read_unweighted_graph(const char* fname, bool is_symmetric,
+                                                                        bool mmap = false)
+{
+    (void)is_symmetric;
+    (void)mmap;
+    uint64_t n = 0, m = 0;
+    wharf::check(wharf_read_adjacency_graph(fname, &n, &m, nullptr, nullptr), nullptr, "read_unweighted_graph");
+    std::cout << "Vertices: " << n << " Edges: " << m << std::endl;
+    auto* off = pbbs::new_array_no_init<uintE>(n);
+    auto* adj = pbbs::new_array_no_init<uintV>(m);
+    wharf::check(wharf_read_adjacency_graph(fname, &n, &m, off, adj), nullptr, "read_unweighted_graph");
+    return std::make_tuple((size_t)n, (size_t)m, off, adj);
+}
+
+#define dygrl dynamic_graph_representation_learning_with_metropolis_hastings
+
+namespace dygrl {
+
+// graph/wharfmh.h:21 — the reference's class, same constructors and methods
+class WharfMH {
+public:
+    using Edge = std::tuple<uintV, uintV>;
+
+    // WharfMH(long n, long m) (wharfmh.h:26): n isolated vertices
+    WharfMH(long graph_vertices, long graph_edges) : w_((sync_config(), graph_vertices), graph_edges) {}
+
+    // WharfMH(n, m, offsets, edges, free_memory) (wharfmh.h:58-110): the CSR is
+    // copied to the GPU; with free_memory the arrays are released afterwards,
+    // as the reference's pbbs::free_array does (wharfmh.h:99-103)
+    WharfMH(long graph_vertices, long graph_edges, uintE* offsets, uintV* edges, bool free_memory = true)
+        : w_((sync_config(), graph_vertices), graph_edges, offsets, edges)
+    {
+        if (free_memory) {
+            pbbs::free_array(offsets);
+            pbbs::free_array(edges);
+        }
+    }
+
+    size_t number_of_vertices() const { return w_.number_of_vertices(); }
+    size_t number_of_edges() const { return w_.number_of_edges(); }
+    void generate_initial_random_walks() { w_.generate_initial_random_walks(); }
+
+    // wharfmh.h:439 / 588.  The batch is sorted by source in the caller's buffer
+    // when not `sorted` (the reference sorts it in place too).  `nn` is the
+    // reference's radix-sort key width hint and `run_seq` its sequential-pack
+    // flag: neither changes the result, and the device sort needs neither.
+    // Returns the affected walk ids (ascending); with apply_walk_updates ==
+    // false, like the reference (wharfmh.h:547-548), a sequence of that many
+    // entries that are not filled in (zeros here).
+    pbbs::sequence<types::WalkID> insert_edges_batch(size_t m, Edge* edges, bool sorted = false,
+                                                     bool remove_dups = false,
+                                                     size_t nn = std::numeric_limits<size_t>::max(),
+                                                     bool apply_walk_updates = true, bool run_seq = false)
+    {
+        return update(true, m, edges, sorted, remove_dups, nn, apply_walk_updates, run_seq);
+    }
+    pbbs::sequence<types::WalkID> delete_edges_batch(size_t m, Edge* edges, bool sorted = false,
+                                                     bool remove_dups = false,
+                                                     size_t nn = std::numeric_limits<size_t>::max(),
+                                                     bool apply_walk_updates = true, bool run_seq = false)
+    {
+        return update(false, m, edges, sorted, remove_dups, nn, apply_walk_updates, run_seq);
+    }
+
+    // batch_walk_update (wharfmh.h:733): the reference takes the MapOfChanges
+    // its update computed; here its vertex set (e.g. the sources of a batch
+    // applied with apply_walk_updates = false) — see wharf_batch_walk_update
+    pbbs::sequence<types::WalkID> batch_walk_update(const std::vector<types::Vertex>& sources)
+    {
+        std::vector<uint32_t> ids(std::max<uint64_t>(walks(), 1));
+        uint64_t na = 0;
+        wharf::check(wharf_batch_walk_update(w_.handle(), sources.data(), sources.size(), 0, ids.data(), &na),
+                     w_.handle(), "batch_walk_update");
+        ids.resize(na);
+        return pbbs::sequence<types::WalkID>(std::move(ids));
+    }
+
+    std::string walk(types::WalkID walk_id) { return w_.walk(walk_id); }
+    types::Vertex vertex_at_walk(types::WalkID walk_id, types::Position position)
+    {
+        return w_.vertex_at_walk(walk_id, position);
+    }
+    void destroy() { w_.destroy(); }
+    void destroy_index() { w_.destroy_index(); }
+    void memory_footprint() const { (void)w_.memory_footprint(); }
+
+    wharf::WharfMH& engine() { return w_; }   // the full C++ mirror (exports, stats, shards)
+
+private:
+    // config::* -> the configuration the next handle is created with
+    static int sync_config()
+    {
+        wharf_config& c = wharf::config();
+        c.walks_per_vertex = config::walks_per_vertex;
+        c.walk_length = config::walk_length;
+        c.model = (int32_t)config::random_walk_model;
+        c.paramP = config::paramP;
+        c.paramQ = config::paramQ;
+        c.sampler_init = (int32_t)config::sampler_init_strategy;
+        c.deterministic = config::deterministic_mode ? 1 : 0;
+        c.seed = config::seed;
+        return 0;
+    }
+
+    uint64_t walks() const
+    {
+        uint64_t w = 0;
+        wharf::check(wharf_shard(w_.handle(), nullptr, nullptr, &w), w_.handle(), "shard");
+        return w;
+    }
+
+    pbbs::sequence<types::WalkID> update(bool insert, size_t m, Edge* edges, bool sorted, bool remove_dups,
+                                         size_t nn, bool apply, bool run_seq)
+    {
+        auto ids = insert ? w_.insert_edges_batch(m, edges, sorted, remove_dups, nn, apply, run_seq)
+                          : w_.delete_edges_batch(m, edges, sorted, remove_dups, nn, apply, run_seq);
+        const wharf_stats st = w_.stats();
+        (insert ? graph_update_time_on_insert : graph_update_time_on_delete).add(st.last_graph_update_ms * 1e-3);
+        if (apply) (insert ? walk_update_time_on_insert : walk_update_time_on_delete).add(st.last_walk_update_ms * 1e-3);
+        if (!apply) std::fill(ids.begin(), ids.end(), 0u);
+        return pbbs::sequence<types::WalkID>(std::move(ids));
+    }
+
+    wharf::WharfMH w_;
+};
+
+}  // namespace dygrl

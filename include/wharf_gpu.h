@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define WHARF_ABI_VERSION 2
+#define WHARF_ABI_VERSION 3
 
 enum {
     WHARF_OK = 0,
@@ -125,6 +125,18 @@ int wharf_insert_edges(wharf_handle* h, uint64_t m, const uint32_t* pairs, uint3
                        uint32_t* affected_out, uint64_t* n_affected);
 int wharf_delete_edges(wharf_handle* h, uint64_t m, const uint32_t* pairs, uint32_t flags,
                        uint32_t* affected_out, uint64_t* n_affected);
+
+/* WharfMH::batch_walk_update (wharfmh.h:733-923) on its own: re-walk every owned
+ * walk from its first position holding one of the k `sources` (the vertex set
+ * of the reference's MapOfChanges, wharfmh.h:519-537), on the current graph.
+ * Samplers are not reset (the reference resets them in insert/delete,
+ * wharfmh.h:504,539,652,689), and MH draws are keyed by the epoch of the last
+ * applied batch, so insert_edges(flags without WHARF_APPLY_WALK_UPDATES)
+ * followed by batch_walk_update(that batch's sources) gives exactly the walks
+ * of insert_edges(WHARF_APPLY_WALK_UPDATES).  flags: WHARF_AFFECTED_DEVICE
+ * only; affected_out / n_affected as for wharf_insert_edges. */
+int wharf_batch_walk_update(wharf_handle* h, const uint32_t* sources, uint64_t k, uint32_t flags,
+                            uint32_t* affected_out, uint64_t* n_affected);
 
 /* number_of_vertices / number_of_edges (wharfmh.h:117-133). */
 int wharf_number_of_vertices(const wharf_handle* h, uint64_t* n);

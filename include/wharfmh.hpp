@@ -60,8 +60,10 @@ public:
     }
 
     // WharfMH(long n, long m, uintE* offsets, uintV* edges, bool free_memory) (wharfmh.h:58).
-    // The arrays are copied; free_memory is accepted for source compatibility but
-    // the caller keeps ownership (the reference frees them with pbbs::free_array).
+    // The arrays are copied and the caller keeps ownership here; free_memory is
+    // accepted for source compatibility.  include/compat/wharfmh.h's
+    // dygrl::WharfMH takes ownership and frees them, as the reference does
+    // with pbbs::free_array (wharfmh.h:99-103).
     WharfMH(long graph_vertices, long graph_edges, const uint64_t* offsets, const uint32_t* edges,
             bool free_memory = true, int device = 0)
     {
@@ -105,6 +107,19 @@ public:
                                              bool run_seq = false)
     {
         return update(false, m, edges, sorted, remove_dups, nn, apply_walk_updates, run_seq);
+    }
+
+    // batch_walk_update (wharfmh.h:733) over a vertex set (wharf_batch_walk_update)
+    std::vector<uint32_t> batch_walk_update(const std::vector<uint32_t>& sources)
+    {
+        uint64_t walks = 0;
+        check(wharf_shard(h_, nullptr, nullptr, &walks), h_, "shard");
+        std::vector<uint32_t> affected(std::max<uint64_t>(walks, 1));
+        uint64_t na = 0;
+        check(wharf_batch_walk_update(h_, sources.data(), sources.size(), 0, affected.data(), &na), h_,
+              "batch_walk_update");
+        affected.resize(na);
+        return affected;
     }
 
     // walk (wharfmh.h:365): "v0 v1 ... " with a trailing space

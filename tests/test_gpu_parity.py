@@ -278,6 +278,54 @@ def test_rmat_scale14_stream_vs_oracle(W):
     _compare_stream(W, off, adj, batches, wpv=10, L=80)
 
 
+@pytest.mark.parametrize("mode", ["det", "deepwalk", "node2vec"])
+def test_batch_walk_update_deferred_equals_applied(W, mode):
+    """wharf_batch_walk_update (wharfmh.h:733): an update with
+    apply_walk_updates=False followed by batch_walk_update(the batch's sources)
+    gives the walks and affected ids of the applied update, which equal the
+    oracle's; a standalone call over a vertex set equals an update whose batch
+    has those sources and changes no edge (deterministic: same draws)."""
+    base = O.generate_batch_of_edges(40000, 1 << 12, 31, False, False)
+    off, adj = O.csr_from_edges(1 << 12, base)
+    kw = dict(deterministic=True) if mode == "det" else dict(
+        deterministic=False, seed=11, model=1 if mode == "node2vec" else 0, paramP=0.5, paramQ=2.0)
+    cfg = W.WharfConfig(walks_per_vertex=4, walk_length=40, **kw)
+    ga = W.WharfMH.from_csr(off, adj, config=cfg)
+    gd = W.WharfMH.from_csr(off, adj, config=cfg)
+    ref = O.Engine(off, adj, wpv=4, L=40, model=cfg.model, p=cfg.paramP, q=cfg.paramQ, init=cfg.sampler_init,
+                   deterministic=cfg.deterministic, seed=cfg.seed)
+    for g in (ga, gd):
+        g.generate_initial_random_walks()
+    ref.generate()
+    for s, ins in ((41, True), (42, False), (43, True)):
+        b = O.generate_batch_of_edges(600, 1 << 12, s, False, False)
+        fa = ga.insert_edges_batch if ins else ga.delete_edges_batch
+        fd = gd.insert_edges_batch if ins else gd.delete_edges_batch
+        aa = fa(b, remove_dups=True)
+        fd(b, remove_dups=True, apply_walk_updates=False)
+        ad = gd.batch_walk_update(b[:, 0][::-1])          # any order, duplicates allowed
+        ar = ref.update(ins, b, O.REMOVE_DUPS | O.APPLY_WALK_UPDATES)
+        np.testing.assert_array_equal(aa, ar)
+        np.testing.assert_array_equal(ad, aa)
+        np.testing.assert_array_equal(gd.walks(), ga.walks())
+        np.testing.assert_array_equal(ga.walks(), ref.walks())
+        assert gd.stats()["steps"] == ga.stats()["steps"] == ref.steps
+    if mode == "det":
+        # standalone: sources S, graph unchanged == an insert of existing edges out of S
+        o2, a2 = ga.flatten_graph()
+        S = np.array([v for v in range(0, 1 << 12, 37) if o2[v + 1] > o2[v]], np.uint32)
+        ex = np.stack([S, a2[o2[S].astype(np.int64)]], axis=1).astype(np.uint32)
+        ad = gd.batch_walk_update(S)
+        ar = ref.update(True, ex, O.REMOVE_DUPS | O.APPLY_WALK_UPDATES)
+        np.testing.assert_array_equal(ad, ar)
+        np.testing.assert_array_equal(gd.walks(), ref.walks())
+    assert len(gd.batch_walk_update(np.zeros(0, np.uint32))) == 0
+    with pytest.raises(RuntimeError):
+        gd.batch_walk_update(np.array([1 << 12], np.uint32))
+    ga.destroy()
+    gd.destroy()
+
+
 def test_affected_ids_on_device_match_host_list(W):
     """WHARF_AFFECTED_DEVICE: ids written to HBM equal the host list and the oracle's."""
     import torch
