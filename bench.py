@@ -245,7 +245,7 @@ def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrie
            "mean_rewalk_steps_rank0": int(np.mean(rsteps)),
            "rewalk_Gsteps_per_s": round(float(np.sum(rsteps) / np.sum(kern) / 1e6), 2),
            "generation_same_graph": gen3,
-           "median_csr_move_ms": round(float(np.median(mv)), 4), "moved_slots": int(np.median(mslots)),
+           "median_in_edge_scan_ms": round(float(np.median(mv)), 4), "pool_slots": int(np.median(mslots)),
            "stored_positions_rank0": int(gs.number_of_walks) * args.length,
            "record_bytes": 32 if (cfg.model == W.NODE2VEC and not cfg.deterministic) else 16}
     if scan:
@@ -322,7 +322,8 @@ def streaming_rooflines(rewalk, rewalk_det):
     algorithmic bytes (SURVEY 8(d)): rewalk-point scan 4 B per stored position;
     deterministic re-walk (suffix table + chunked copy) 4 B per stored position
     (each position is read up to the walk's rewalk point and written after it);
-    CSR move 2 x (4 B target + record) per old slot."""
+    in-edge record scan of the slack-row CSR update 4 B per pool slot (the
+    slots' targets are read; the few records of sources' in-edges written)."""
     out = {}
     def ent(kernel, bytes_, ms, per):
         if not ms:
@@ -338,9 +339,8 @@ def streaming_rooflines(rewalk, rewalk_det):
                                                rewalk_det["median_rewalk_kernel_ms"], "4 B per stored position")
     src = rewalk or rewalk_det
     if src:
-        per = 2 * (4 + src["record_bytes"])
-        out["csr_move"] = ent("k_move_edges (record patch into the second buffer)", per * src["moved_slots"],
-                              src["median_csr_move_ms"], f"{per} B per old CSR slot")
+        out["in_edge_scan"] = ent("k_patch_in_edges (records of the batch sources' in-edges)", 4 * src["pool_slots"],
+                                  src["median_in_edge_scan_ms"], "4 B per pool slot")
     return out or None
 
 

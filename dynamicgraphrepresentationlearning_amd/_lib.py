@@ -61,6 +61,10 @@ class wharf_stats(C.Structure):
         ("hbm_bytes_graph", C.c_uint64),
         ("last_csr_move_ms", C.c_double),
         ("last_moved_slots", C.c_uint64),
+        ("pool_slots", C.c_uint64),
+        ("pool_capacity", C.c_uint64),
+        ("last_moved_row_slots", C.c_uint64),
+        ("repacks", C.c_uint64),
     ]
 
 

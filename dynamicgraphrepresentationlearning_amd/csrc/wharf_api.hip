@@ -85,13 +85,17 @@ struct wharf_handle {
     uint32_t L = 0, wpv = 0;
     bool anchors = false, has_walks = false;
     uint32_t epoch = 0;
-    DevBuf off, adj, vrec, erec, row_epoch, off2, adj2, anchor2, ehash, erec2;
+    // slack-row CSR: row v = slots [off[v], off[v] + deg[v]) of the pool (adj, erec), cap[v] reserved
+    DevBuf off, adj, deg, cap, vrec, erec, row_epoch, ehash;
+    DevBuf off2, adj2, erec2;                  // temporaries: contiguous CSR at creation, repack, export
+    uint64_t pool_used = 0, pool_cap = 0;      // slots handed out / allocated
+    uint64_t repacks = 0, grown = 0;           // pool repacks so far; slots handed to rows moved by the last batch
     uint64_t ehash_mask = 0, ehash_used = 0;   // capacity - 1; occupied slots incl. tombstones
     DevBuf fdir, fpool, fplan;                 // node2vec MH: per-row neighbour filters (k_filter_*)
     DevBuf memo, srcidx;                       // deterministic re-walk: suffix table, source index
     uint64_t fpool_used = 0;                   // words handed out (rows that outgrew theirs leave gaps)
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
-    DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, rtabs, count, pairs, sel, defer, esave;
+    DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, count, pairs, sel, defer, rplan, pscan, scratch;
     wharf_stats st{};
     std::string err;
 
@@ -131,14 +135,99 @@ struct wharf_handle {
         return res;
     }
 
-    // CSR (off, adj) from the sorted unique keys in k1
+    // slots the pool holds for `used` handed-out slots: 1/16 headroom (rows that
+    // outgrow their slack move to its end) plus `extra`; none with
+    // WHARF_POOL_NO_HEADROOM=1 (tests: every moved row repacks the pool)
+    static uint64_t pool_capacity(uint64_t used, uint64_t extra)
+    {
+        const char* nh = getenv("WHARF_POOL_NO_HEADROOM");
+        const uint64_t head = nh && atoi(nh) ? 0 : std::max<uint64_t>(used >> 4, 1ull << 16);
+        return used + head + extra;
+    }
+    // WHARF_NO_ROW_SLACK=1 (tests): rows get no slack, so every growing row moves
+    static int row_slack()
+    {
+        const char* ns = getenv("WHARF_NO_ROW_SLACK");
+        return ns && atoi(ns) ? 0 : 1;
+    }
+
+    // CSR from the sorted unique keys in k1: contiguous in off2/adj2, then laid
+    // out as slack rows
     void csr_from_keys(uint64_t mm)
     {
-        off.ensure((n + 1) * 8);
-        adj.ensure(std::max<uint64_t>(mm, 1) * 4, true);   // slack: insert batches grow it in place
-        launch_offsets_from_keys(k1.as<uint64_t>(), mm, n, off.as<uint64_t>(), s);
-        launch_low32(k1.as<uint64_t>(), mm, adj.as<uint32_t>(), s);
+        off2.ensure((n + 1) * 8);
+        adj2.ensure(std::max<uint64_t>(mm, 1) * 4);
+        launch_offsets_from_keys(k1.as<uint64_t>(), mm, n, off2.as<uint64_t>(), s);
+        launch_low32(k1.as<uint64_t>(), mm, adj2.as<uint32_t>(), s);
         m = mm;
+        layout_rows();
+        off2.release();
+        adj2.release();
+    }
+
+    // contiguous CSR (off2, adj2) -> slack rows (off, deg, cap, adj); the
+    // capacities are scanned as u64 in off itself
+    void layout_rows()
+    {
+        deg.ensure(std::max<uint64_t>(n, 1) * 4);
+        cap.ensure(std::max<uint64_t>(n, 1) * 4);
+        off.ensure((n + 1) * 8);
+        DevBuf capw;
+        capw.ensure((n + 1) * 8);
+        launch_row_degrees(off2.as<uint64_t>(), n, deg.as<uint32_t>(), cap.as<uint32_t>(), capw.as<uint64_t>(),
+                           row_slack(), s);
+        scan_u64(capw.as<uint64_t>(), off.as<uint64_t>(), n + 1);
+        HIPCHK(hipMemcpyAsync(&pool_used, off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+        sync();
+        capw.release();
+        pool_cap = pool_capacity(pool_used, 0);
+        adj.release();
+        adj.ensure(std::max<uint64_t>(pool_cap, 1) * 4);
+        HIPCHK(hipMemsetAsync(adj.p, 0xFF, std::max<uint64_t>(pool_cap, 1) * 4, s));   // kGap
+        launch_copy_rows(off2.as<uint64_t>(), deg.as<uint32_t>(), adj2.as<uint32_t>(), off.as<uint64_t>(), n,
+                         adj.as<uint32_t>(), nullptr, nullptr, s);
+    }
+
+    // Fresh slack for every row, in a new pool with room for `extra` more slots
+    // (the pool ran out of headroom): rows, their anchor entries and records
+    // move; the records are rebuilt (every row offset changed).
+    void repack(uint64_t extra)
+    {
+        const uint64_t rs = rec_stride();
+        DevBuf capw;
+        capw.ensure((n + 1) * 8);
+        launch_row_recap(deg.as<uint32_t>(), n, cap.as<uint32_t>(), capw.as<uint64_t>(), row_slack(), s);
+        off2.ensure((n + 1) * 8);
+        scan_u64(capw.as<uint64_t>(), off2.as<uint64_t>(), n + 1);
+        uint64_t used = 0;
+        HIPCHK(hipMemcpyAsync(&used, off2.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+        sync();
+        capw.release();
+        const uint64_t pc = pool_capacity(used, extra);
+        adj2.ensure(std::max<uint64_t>(pc, 1) * 4);
+        HIPCHK(hipMemsetAsync(adj2.p, 0xFF, std::max<uint64_t>(pc, 1) * 4, s));
+        erec2.ensure(std::max<uint64_t>(pc, 1) * sizeof(ERec) * rs);
+        launch_copy_rows(off.as<uint64_t>(), deg.as<uint32_t>(), adj.as<uint32_t>(), off2.as<uint64_t>(), n,
+                         adj2.as<uint32_t>(), anchors ? erec.as<uint64_t>() + 2 : nullptr,
+                         anchors ? erec2.as<uint64_t>() + 2 : nullptr, s);
+        std::swap(off, off2);
+        std::swap(adj, adj2);
+        std::swap(erec, erec2);
+        off2.release();
+        adj2.release();
+        erec2.release();
+        pool_used = used;
+        pool_cap = pc;
+        launch_vrec(off.as<uint64_t>(), deg.as<uint32_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
+        launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rs, 1, s);
+        repacks++;
+    }
+
+    void scan_u64(uint64_t* in, uint64_t* out, uint64_t cnt)
+    {
+        rp([&](void* t, size_t& b) {
+            return rocprim::exclusive_scan(t, b, in, out, (uint64_t)0, (size_t)cnt, rocprim::plus<uint64_t>(), s);
+        });
     }
 
     void finish_graph()
@@ -170,9 +259,10 @@ struct wharf_handle {
     void build_records()
     {
         vrec.ensure(std::max<uint64_t>(n, 1) * sizeof(ERec));
-        erec.ensure(std::max<uint64_t>(m, 1) * sizeof(ERec) * rec_stride(), true);
-        launch_vrec(off.as<uint64_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
-        launch_erec(adj.as<uint32_t>(), m, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rec_stride(), s);
+        erec.release();
+        erec.ensure(std::max<uint64_t>(pool_cap, 1) * sizeof(ERec) * rec_stride());
+        launch_vrec(off.as<uint64_t>(), deg.as<uint32_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
+        launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rec_stride(), 0, s);
     }
 
     void build_edge_hash()
@@ -183,7 +273,8 @@ struct wharf_handle {
         ehash_mask = cap - 1;
         ehash_used = m;
         launch_fill_u64(ehash.as<uint64_t>(), cap, kEmptyKey, s);
-        launch_edge_hash_build(off.as<uint64_t>(), n, adj.as<uint32_t>(), ehash.as<uint64_t>(), ehash_mask, s);
+        launch_edge_hash_build(off.as<uint64_t>(), deg.as<uint32_t>(), n, adj.as<uint32_t>(), ehash.as<uint64_t>(),
+                               ehash_mask, s);
     }
 
     // neighbour filters of every row: sizes, directory (exclusive scan), fill;
@@ -195,7 +286,7 @@ struct wharf_handle {
         DevBuf words;
         words.ensure((n + 1) * 8);
         fdir.ensure((n + 1) * 8);
-        launch_filter_sizes(off.as<uint64_t>(), n, words.as<uint64_t>(), s);
+        launch_filter_sizes(deg.as<uint32_t>(), n, words.as<uint64_t>(), s);
         uint64_t* in = words.as<uint64_t>();
         uint64_t* out = fdir.as<uint64_t>();
         rp([&](void* t, size_t& b) {
@@ -212,8 +303,9 @@ struct wharf_handle {
         fpool.ensure(want);
         fpool_used = total;
         HIPCHK(hipMemsetAsync(fpool.p, 0, total * 4, s));
-        launch_filter_pack(off.as<uint64_t>(), n, fdir.as<uint64_t>(), s);
-        launch_filter_fill(off.as<uint64_t>(), n, adj.as<uint32_t>(), fdir.as<uint64_t>(), fpool.as<uint32_t>(), s);
+        launch_filter_pack(deg.as<uint32_t>(), n, fdir.as<uint64_t>(), s);
+        launch_filter_fill(off.as<uint64_t>(), deg.as<uint32_t>(), n, adj.as<uint32_t>(), fdir.as<uint64_t>(),
+                           fpool.as<uint32_t>(), s);
     }
 
     // after a batch: rebuild the filters of the k batch sources from their new rows
@@ -223,7 +315,7 @@ struct wharf_handle {
         fplan.ensure((k + 1) * 16);
         uint64_t* need = fplan.as<uint64_t>();
         uint64_t* gofs = need + k + 1;
-        launch_filter_plan(runs_d, k, off.as<uint64_t>(), fdir.as<uint64_t>(), need, s);
+        launch_filter_plan(runs_d, k, deg.as<uint32_t>(), fdir.as<uint64_t>(), need, s);
         rp([&](void* t, size_t& b) {
             return rocprim::exclusive_scan(t, b, need, gofs, (uint64_t)0, (size_t)(k + 1), rocprim::plus<uint64_t>(), s);
         });
@@ -234,7 +326,7 @@ struct wharf_handle {
             build_filters();   // out of headroom: re-size and re-fill every row (drops the gaps)
             return;
         }
-        launch_filter_rows(runs_d, k, off.as<uint64_t>(), adj.as<uint32_t>(), need, gofs, fpool_used,
+        launch_filter_rows(runs_d, k, off.as<uint64_t>(), deg.as<uint32_t>(), adj.as<uint32_t>(), need, gofs, fpool_used,
                            fdir.as<uint64_t>(), fpool.as<uint32_t>(), s);
         fpool_used += grow;
     }
@@ -368,9 +460,11 @@ void free_handle(wharf_handle* h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->s) (void)hipStreamSynchronize(h->s);
-    for (DevBuf* b : {&h->off, &h->adj, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->fdir, &h->fpool, &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->anchor2, &h->walks,
-                      &h->aff, &h->rtab, &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags,
-                      &h->chg, &h->cf, &h->runstart, &h->runs, &h->rtabs, &h->count, &h->pairs, &h->sel, &h->defer, &h->esave})
+    for (DevBuf* b : {&h->off, &h->adj, &h->deg, &h->cap, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->fdir, &h->fpool,
+                      &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->walks, &h->aff, &h->rtab,
+                      &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags, &h->chg, &h->cf,
+                      &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel, &h->defer, &h->rplan, &h->pscan,
+                      &h->scratch})
         b->release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -383,6 +477,9 @@ void build_graph_from_keys(wharf_handle* h, uint64_t cnt, bool drop_loops)
 {
     const uint64_t mm = h->unique_keys(cnt, drop_loops, 32 + std::max<uint32_t>(bits_for(h->n), 1));
     h->csr_from_keys(mm);
+    // the keys and sort temporaries are done with: free them before the records
+    // (configs[4]: 2 x 29 GB of keys next to 131 GB of 32-B records)
+    for (DevBuf* b : {&h->k1, &h->k2, &h->tmp, &h->flags}) b->release();
     h->finish_graph();
 }
 
@@ -522,7 +619,8 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->chg.ensure((mb + 1) * 4);
         h->cf.ensure((mb + 1) * 4);
         HIPCHK(hipMemsetAsync(h->chg.as<uint32_t>() + mb, 0, 4, s));
-        launch_batch_change(bkeys, mb, h->off.as<uint64_t>(), h->adj.as<uint32_t>(), insert, h->chg.as<uint32_t>(), s);
+        launch_batch_change(bkeys, mb, h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->adj.as<uint32_t>(), insert,
+                            h->chg.as<uint32_t>(), s);
         {
             uint32_t* in = h->chg.as<uint32_t>();
             uint32_t* out = h->cf.as<uint32_t>();
@@ -536,88 +634,64 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         HIPCHK(hipMemcpyAsync(&total_chg, h->cf.as<uint32_t>() + mb, 4, hipMemcpyDeviceToHost, s));
         h->sync();
 
-        // 4. new CSR: offsets, moved old edges, placed new edges; samplers of
-        //    the batch sources are reset (wharfmh.h:504-540, 652-690)
+        // 4. the batch sources' rows (wharfmh.h:504-540, 652-690): merged in place
+        //    or moved to the pool's end; their samplers are reset (row epoch)
         const uint64_t m_new = insert ? h->m + total_chg : h->m - total_chg;
         // row epochs live in 24 bits of the records (wharf_device.h make_rec) and
         // feed the Philox counters: refuse the batch that would wrap them
         REQUIRE(h->epoch + 1 < (1u << kEpochBits), WHARF_E_INVALID, "update epoch limit (2^24 applied batches) reached");
         h->epoch++;
         h->runs.ensure(k * sizeof(RunInfo));
-        HIPCHK(hipMemsetAsync(h->bitmap.p, 0, (h->bitmap_words() + kBloomWords) * 4, s));
-        launch_run_info(bkeys, h->runstart.as<uint32_t>(), k, mb, h->off.as<uint64_t>(), h->runs.as<RunInfo>(),
-                        h->bitmap.as<uint32_t>(), h->bitmap.as<uint32_t>() + h->bitmap_words(),
-                        h->row_epoch.as<uint32_t>(), h->epoch, s);
-        h->off2.ensure((h->n + 1) * 8);
-        h->adj2.ensure(std::max<uint64_t>(m_new, 1) * 4, true);
-        RunIndex rx;
-        h->rtabs.ensure(run_tables_words(h->n, h->m) * 4);
-        launch_run_tables(h->runs.as<RunInfo>(), k, h->cf.as<uint32_t>(), mb, h->n, h->m, h->rtabs.as<uint32_t>(), &rx, s);
-        launch_new_offsets(h->off.as<uint64_t>(), h->n, rx, h->cf.as<uint32_t>(), mb, insert, h->off2.as<uint64_t>(), s);
-        // Edge records (node2vec MH: with their anchor entries) move with their
-        // slot and are patched arithmetically: into a second record buffer when
-        // it fits, else in place (chunked, k_move_records_inplace) when the
-        // buffer has room for m_new; else they are rebuilt by a gather and the
-        // anchors travel through a separate 8-B-per-slot buffer.
-        // WHARF_FORCE_RECORD_REBUILD (tests): 1 = no second buffer, 2 = gather.
-        const uint64_t rs = h->rec_stride();
-        const uint64_t rec_bytes = std::max<uint64_t>(m_new, 1) * sizeof(ERec) * rs;
-        const char* force = getenv("WHARF_FORCE_RECORD_REBUILD");
-        const int forced = force ? atoi(force) : 0;
-        enum { kPatch, kInPlace, kGather } path = forced ? kInPlace : kPatch;
-        if (path == kPatch) {
-            try {
-                h->erec2.ensure(rec_bytes, true);
-            } catch (const WharfError&) {
-                (void)hipGetLastError();
-                path = kInPlace;
-            }
+        h->rplan.ensure(k * sizeof(RowPlan));
+        h->pscan.ensure((k + 1) * 32);
+        uint64_t* need = h->pscan.as<uint64_t>();
+        uint64_t* save = need + (k + 1);
+        uint64_t* relofs = save + (k + 1);
+        uint64_t* sofs = relofs + (k + 1);
+        const int slack = wharf_handle::row_slack();
+        uint64_t grow = 0, saved = 0;
+        for (int attempt = 0;; attempt++) {
+            HIPCHK(hipMemsetAsync(h->bitmap.p, 0, (h->bitmap_words() + kBloomWords) * 4, s));
+            launch_run_info(bkeys, h->runstart.as<uint32_t>(), k, mb, h->off.as<uint64_t>(), h->deg.as<uint32_t>(),
+                            h->runs.as<RunInfo>(), h->bitmap.as<uint32_t>(), h->bitmap.as<uint32_t>() + h->bitmap_words(),
+                            h->row_epoch.as<uint32_t>(), h->epoch, s);
+            launch_plan_rows(h->runs.as<RunInfo>(), k, h->cap.as<uint32_t>(), h->cf.as<uint32_t>(), insert, slack, need,
+                             save, h->rplan.as<RowPlan>(), s);
+            h->scan_u64(need, relofs, k + 1);
+            h->scan_u64(save, sofs, k + 1);
+            HIPCHK(hipMemcpyAsync(&grow, relofs + k, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(&saved, sofs + k, 8, hipMemcpyDeviceToHost, s));
+            h->sync();
+            if (h->pool_used + grow <= h->pool_cap) break;
+            REQUIRE(attempt == 0, WHARF_E_STATE,
+                    "slot pool exhausted after a repack (used " + std::to_string(h->pool_used) + ", grow " +
+                        std::to_string(grow) + ", capacity " + std::to_string(h->pool_cap) + ")");
+            // out of headroom: fresh slack everywhere, then plan again.  The fresh
+            // capacities can be smaller than the old ones (rows that shrank keep
+            // theirs), so room is made for every source moving with grown slack.
+            const uint64_t all = saved + (insert ? total_chg : 0);
+            h->repack(all + all / 8 + 4 * k);
         }
-        if (path == kInPlace && (forced == 2 || h->erec.cap < rec_bytes)) path = kGather;
-        if (path == kInPlace) {
-            const uint64_t C = inplace_chunk(total_chg);
-            try {
-                h->esave.ensure(std::max<uint64_t>((h->m + C - 1) / C * total_chg, 1) * sizeof(ERec) * rs);
-            } catch (const WharfError&) {
-                (void)hipGetLastError();
-                path = kGather;
-            }
-        }
-        if (path == kGather && h->anchors) h->anchor2.ensure(std::max<uint64_t>(m_new, 1) * 8, true);
-        uint64_t* anc_in = h->anchors ? h->erec.as<uint64_t>() + 2 : nullptr;
-        uint64_t* anc_out = !h->anchors || path == kInPlace ? nullptr
-                            : path == kPatch ? h->erec2.as<uint64_t>() + 2 : h->anchor2.as<uint64_t>();
-        const uint32_t as_out = path == kPatch ? (uint32_t)kAnchorStride : 1u;
-        const uint64_t m_old = h->m;
-        HIPCHK(hipEventRecord(h->ev[4], s));
-        launch_move_edges(h->adj.as<uint32_t>(), anc_in, kAnchorStride, m_old, rx, bkeys, h->cf.as<uint32_t>(),
-                          h->off2.as<uint64_t>(), insert, h->adj2.as<uint32_t>(), anc_out, as_out, m_new,
-                          path == kPatch ? h->erec.as<ERec>() : nullptr, path == kPatch ? h->erec2.as<ERec>() : nullptr,
-                          (uint32_t)rs, mb, h->epoch, s);
-        HIPCHK(hipEventRecord(h->ev[5], s));
-        h->st.last_moved_slots = m_old;
-        if (insert)   // (the records of source rows, new slots included, are rebuilt below)
-            launch_place_new(bkeys, mb, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(), h->runstart.as<uint32_t>(), k,
-                             h->runs.as<RunInfo>(), h->adj.as<uint32_t>(), h->off2.as<uint64_t>(),
-                             h->adj2.as<uint32_t>(), path == kGather ? anc_out : nullptr, 1u, m_new, s);
-        std::swap(h->off, h->off2);
-        std::swap(h->adj, h->adj2);
+        h->grown = grow;
+        h->scratch.ensure(std::max<uint64_t>(saved, 1) * 4);
+        const uint32_t rs = (uint32_t)h->rec_stride();
+        launch_save_rows(h->runs.as<RunInfo>(), k, h->adj.as<uint32_t>(), sofs, h->scratch.as<uint32_t>(), s);
+        launch_merge_rows(h->runs.as<RunInfo>(), k, bkeys, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(),
+                          h->scratch.as<uint32_t>(), sofs, relofs, h->pool_used, insert, h->rplan.as<RowPlan>(),
+                          h->adj.as<uint32_t>(), s);
+        launch_commit_rows(h->runs.as<RunInfo>(), k, h->rplan.as<RowPlan>(), h->epoch, h->off.as<uint64_t>(),
+                           h->deg.as<uint32_t>(), h->cap.as<uint32_t>(), h->vrec.as<ERec>(), s);
+        h->pool_used += grow;
         h->m = m_new;
-        if (path == kPatch || path == kInPlace) {
-            if (path == kPatch) {
-                std::swap(h->erec, h->erec2);
-            } else {
-                launch_move_records_inplace(h->erec.as<ERec>(), (uint32_t)rs, m_old, total_chg, h->esave.as<ERec>(), rx,
-                                            h->cf.as<uint32_t>(), mb, insert, h->epoch, s);
-            }
-            launch_vrec(h->off.as<uint64_t>(), h->n, h->row_epoch.as<uint32_t>(), h->vrec.as<ERec>(), s);
-            launch_erec_rows(h->runs.as<RunInfo>(), k, h->off.as<uint64_t>(), h->adj.as<uint32_t>(),
-                             h->vrec.as<ERec>(), h->erec.as<ERec>(), (uint32_t)rs, s);
-        } else {
-            h->erec2.release();
-            h->build_records();
-            if (h->anchors) launch_anchor_merge(h->anchor2.as<uint64_t>(), h->m, h->erec.as<uint64_t>() + 2, s);
-        }
+        // records: the source rows' slots (anchors reset), then every slot whose
+        // target is a source (one streaming scan of the pool)
+        launch_erec_rows(h->runs.as<RunInfo>(), k, h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->adj.as<uint32_t>(),
+                         h->vrec.as<ERec>(), h->erec.as<ERec>(), rs, s);
+        HIPCHK(hipEventRecord(h->ev[4], s));
+        launch_patch_in_edges(h->adj.as<uint32_t>(), h->pool_used, h->bitmap.as<uint32_t>(),
+                              h->bitmap.as<uint32_t>() + h->bitmap_words(), h->vrec.as<ERec>(), h->erec.as<ERec>(), rs, s);
+        HIPCHK(hipEventRecord(h->ev[5], s));
+        h->st.last_moved_slots = h->pool_used;
         if (h->anchors) {
             // the edge set changes by the batch's changing edges only; rebuild when
             // inserts (and tombstones) push the load past 0.6
@@ -699,6 +773,8 @@ int wharf_create(const wharf_config* cfg, uint64_t n, uint64_t m, const uint64_t
         build_graph_from_keys(h, m, false);
         h->k1.release();
         h->k2.release();
+        h->off2.release();
+        h->adj2.release();
     });
     if (rc != WHARF_OK) {
         free_handle(h);
@@ -869,8 +945,18 @@ int wharf_get_graph(wharf_handle* h, uint64_t* offsets_out, uint32_t* targets_ou
 {
     return guarded(h, [&] {
         REQUIRE(h && offsets_out, WHARF_E_INVALID, "null argument");
-        HIPCHK(hipMemcpyAsync(offsets_out, h->off.p, (h->n + 1) * 8, hipMemcpyDeviceToHost, h->s));
-        if (h->m && targets_out) HIPCHK(hipMemcpyAsync(targets_out, h->adj.p, h->m * 4, hipMemcpyDeviceToHost, h->s));
+        // the slack rows, compacted: offsets = scan of the degrees, rows copied
+        DevBuf coff, cadj;
+        coff.ensure((h->n + 1) * 8);
+        launch_deg_u64(h->deg.as<uint32_t>(), h->n, coff.as<uint64_t>(), h->s);
+        h->scan_u64(coff.as<uint64_t>(), coff.as<uint64_t>(), h->n + 1);
+        HIPCHK(hipMemcpyAsync(offsets_out, coff.p, (h->n + 1) * 8, hipMemcpyDeviceToHost, h->s));
+        if (h->m && targets_out) {
+            cadj.ensure(h->m * 4);
+            launch_copy_rows(h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->adj.as<uint32_t>(), coff.as<uint64_t>(),
+                             h->n, cadj.as<uint32_t>(), nullptr, nullptr, h->s);
+            HIPCHK(hipMemcpyAsync(targets_out, cadj.p, h->m * 4, hipMemcpyDeviceToHost, h->s));
+        }
         h->sync();
     });
 }
@@ -1171,17 +1257,17 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     wharf_memory r{};
     r.n = h->n;
     r.m = h->m;
-    r.csr_bytes = h->off.cap + h->adj.cap;
+    r.csr_bytes = h->off.cap + h->adj.cap + h->deg.cap + h->cap.cap;
     r.records_bytes = h->vrec.cap + h->erec.cap;
     r.walks_bytes = h->walks.cap + h->aff.cap;
     const uint64_t anchor_part = h->anchors ? h->erec.cap / 2 : 0;   // bytes 16-31 of the 32-B records
     r.records_bytes -= anchor_part;
     r.samplers_bytes = anchor_part + h->row_epoch.cap;
     r.edge_hash_bytes = h->ehash.cap + h->fdir.cap + h->fpool.cap;
-    r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->anchor2.cap + h->erec2.cap;
+    r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->erec2.cap + h->scratch.cap + h->rplan.cap + h->pscan.cap;
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
-                      h->runs.cap + h->fplan.cap + h->memo.cap + h->srcidx.cap + h->rtabs.cap + h->count.cap + h->pairs.cap + h->sel.cap + h->defer.cap + h->esave.cap + h->rtab.cap +
-                      h->bitmap.cap + h->counters.cap + h->errflag.cap;
+                      h->runs.cap + h->fplan.cap + h->memo.cap + h->srcidx.cap + h->count.cap + h->pairs.cap +
+                      h->sel.cap + h->defer.cap + h->rtab.cap + h->bitmap.cap + h->counters.cap + h->errflag.cap;
     r.total_bytes = r.csr_bytes + r.records_bytes + r.walks_bytes + r.samplers_bytes + r.edge_hash_bytes +
                     r.update_buffers_bytes + r.scratch_bytes;
     *out = r;
@@ -1196,7 +1282,11 @@ int wharf_get_stats(const wharf_handle* h, wharf_stats* out)
     out->m = h->m;
     out->walks = h->W;
     out->hbm_bytes_walks = h->W * h->L * 4;
-    out->hbm_bytes_graph = (h->n + 1) * 8 + h->m * 4 + (h->n + h->m * h->rec_stride()) * sizeof(ERec);
+    out->hbm_bytes_graph = (h->n + 1) * 8 + h->n * 8 + h->pool_cap * 4 + (h->n + h->pool_cap * h->rec_stride()) * sizeof(ERec);
+    out->pool_slots = h->pool_used;
+    out->pool_capacity = h->pool_cap;
+    out->last_moved_row_slots = h->grown;
+    out->repacks = h->repacks;
     return WHARF_OK;
 }
 

@@ -18,6 +18,15 @@ constexpr uint32_t kSent = 0xFFFFFFFEu;        // wharfmh.h:282 (uint32 max - 1)
 constexpr uint32_t kAnchorNone = 0xFFFFFFFFu;  // MH anchor slot not initialised yet
 constexpr uint32_t kNoRewalk = 0xFFu;          // rewalk position "none"
 constexpr uint32_t kBloomWords = 4096;         // batch-source Bloom filter: 2^17 bits (16 KiB, LDS)
+constexpr uint32_t kGap = 0xFFFFFFFFu;         // unused slot of the slack-row pool (not a vertex id)
+
+// Slack-row CSR capacities: a row starts with 1/16 slack (at least 2 slots);
+// a row that outgrew its slots moves to a place with 1/8 slack (at least 4).
+__host__ __device__ __forceinline__ uint32_t row_cap_initial(uint32_t d)
+{
+    return d ? d + ((d >> 4) > 2u ? (d >> 4) : 2u) : 0u;
+}
+__host__ __device__ __forceinline__ uint32_t row_cap_grown(uint32_t d) { return d + ((d >> 3) > 4u ? (d >> 3) : 4u); }
 
 // two 17-bit hashes (k = 2: ~2 % false positives at 10 k sources in 2^17 bits)
 __host__ __device__ __forceinline__ uint32_t bloom_hash(uint32_t x) { return (x * 2654435761u) >> 15; }

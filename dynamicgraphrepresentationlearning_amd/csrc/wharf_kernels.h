@@ -54,66 +54,56 @@ struct WalkArgs {
 };
 
 
-// bucketed lookup tables over the source-run table (k_run_tables)
-struct RunIndex {
-    const RunInfo* runs;
-    uint64_t k;
-    const uint2* vtab;      // [(n >> vs) + 2] {first run, row shift}
-    const uint32_t* etab;   // [(m >> es) + 2]
-    const uint32_t* eshift; // [(m >> es) + 2] clean bucket: 1 << 31 | shift of its slots, else 0
-    uint32_t vs, es;
+// per batch source: the new row (slack-row CSR update, k_plan_rows .. k_commit_rows)
+constexpr uint64_t kRelocate = ~0ull;   // RowPlan.noff before the merge: the row moves to the pool's end
+struct RowPlan {
+    uint64_t noff;         // new row start
+    uint32_t ndeg, ncap;   // new degree and capacity
+    uint32_t ocap, pad;    // old capacity
 };
-// bucket shift so a table over [0, x] has at most ~2^target entries
-inline uint32_t run_table_shift(uint64_t x, uint32_t target)
-{
-    uint32_t b = 0;
-    while (b < 63 && (x >> b) >= (1ull << target)) b++;
-    return b;
-}
-inline uint64_t run_tables_words(uint64_t n, uint64_t m)
-{
-    return 2 * ((n >> run_table_shift(n, 18)) + 2) + 2 * ((m >> run_table_shift(m, 20)) + 2);
-}
 
 unsigned grid_for(uint64_t work, unsigned block);
 unsigned cu_count();
 
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s);
 void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStream_t s);
-void launch_vrec(const uint64_t* off, uint64_t n, const uint32_t* row_epoch, ERec* vrec, hipStream_t s);
-void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s);
-void launch_anchor_merge(const uint64_t* src, uint64_t m, uint64_t* dst, hipStream_t s);
+void launch_vrec(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* row_epoch, ERec* vrec,
+                 hipStream_t s);
+void launch_erec(const uint32_t* adj, uint64_t slots, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anchors,
+                 hipStream_t s);
 void launch_rmat_keys(const RmatParams& p, uint64_t M, int directed, uint64_t* keys, hipStream_t s);
 void launch_pairs_to_keys(const uint32_t* pairs, uint64_t m, uint64_t n, uint64_t* keys, unsigned long long* err, hipStream_t s);
 void launch_csr_to_keys(const uint64_t* off, uint64_t n, const uint32_t* tgt, uint64_t* keys, unsigned long long* err, hipStream_t s);
 void launch_unique_flags(const uint64_t* keys, uint64_t m, int drop_loops, uint8_t* keep, hipStream_t s);
 void launch_offsets_from_keys(const uint64_t* keys, uint64_t m, uint64_t n, uint64_t* off, hipStream_t s);
 void launch_low32(const uint64_t* keys, uint64_t m, uint32_t* out, hipStream_t s);
-void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off, const uint32_t* adj, int insert,
-                         uint32_t* chg, hipStream_t s);
+void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off, const uint32_t* deg, const uint32_t* adj,
+                         int insert, uint32_t* chg, hipStream_t s);
 void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_t s);
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
-                     RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, uint32_t* row_epoch, uint32_t epoch,
-                     hipStream_t s);
+                     const uint32_t* deg, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, uint32_t* row_epoch,
+                     uint32_t epoch, hipStream_t s);
 void launch_mark_sources(const uint32_t* src, uint64_t k, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom,
                          hipStream_t s);
-void launch_run_tables(const RunInfo* runs, uint64_t k, const uint32_t* cf, uint64_t mb, uint64_t n, uint64_t m,
-                       uint32_t* tabs, RunIndex* x, hipStream_t s);
-void launch_new_offsets(const uint64_t* off, uint64_t n, const RunIndex& x, const uint32_t* cf, uint64_t mb, int insert,
-                        uint64_t* noff, hipStream_t s);
-void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint32_t as_in, uint64_t m, const RunIndex& x,
-                       const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
-                       uint64_t* nanc, uint32_t as_out, uint64_t cap, const ERec* oerec, ERec* nerec, uint32_t rs,
-                       uint64_t mb, uint32_t epoch, hipStream_t s);
-uint64_t move_lds_limit();
-uint64_t inplace_chunk(uint64_t S);   // slots per chunk of the in-place record move (the save buffer holds S per chunk)
-void launch_move_records_inplace(ERec* rec, uint32_t rs, uint64_t m, uint64_t S, ERec* save, const RunIndex& x,
-                                 const uint32_t* cf, uint64_t mb, int insert, uint32_t epoch, hipStream_t s);
-void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* nadj, const ERec* vrec,
-                      ERec* erec, uint32_t rs, hipStream_t s);
-void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf,
-                      const uint32_t* run_start, uint64_t k, const RunInfo* runs, const uint32_t* adj,
-                      const uint64_t* noff, uint32_t* nadj, uint64_t* nanc, uint32_t as_out, uint64_t cap, hipStream_t s);
+void launch_row_degrees(const uint64_t* coff, uint64_t n, uint32_t* deg, uint32_t* cap, uint64_t* capw, int slack,
+                        hipStream_t s);
+void launch_row_recap(const uint32_t* deg, uint64_t n, uint32_t* cap, uint64_t* capw, int slack, hipStream_t s);
+void launch_deg_u64(const uint32_t* deg, uint64_t n, uint64_t* out, hipStream_t s);
+void launch_copy_rows(const uint64_t* soff, const uint32_t* deg, const uint32_t* src, const uint64_t* doff, uint64_t n,
+                      uint32_t* dst, const uint64_t* sanc, uint64_t* danc, hipStream_t s);
+void launch_plan_rows(const RunInfo* runs, uint64_t k, const uint32_t* cap, const uint32_t* cf, int insert, int slack,
+                      uint64_t* need, uint64_t* save, RowPlan* plan, hipStream_t s);
+void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* adj, const uint64_t* sofs, uint32_t* scratch,
+                      hipStream_t s);
+void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint64_t* bkeys, const uint32_t* chg, const uint32_t* cf,
+                       const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs, uint64_t pool_end,
+                       int insert, RowPlan* plan, uint32_t* adj, hipStream_t s);
+void launch_commit_rows(const RunInfo* runs, uint64_t k, const RowPlan* plan, uint32_t epoch, uint64_t* off,
+                        uint32_t* deg, uint32_t* cap, ERec* vrec, hipStream_t s);
+void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* off, const uint32_t* deg, const uint32_t* adj,
+                      const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s);
+void launch_patch_in_edges(const uint32_t* adj, uint64_t slots, const uint32_t* bitmap, const uint32_t* bloom,
+                           const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s);
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s);
 void launch_gather_walk(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* out, hipStream_t s);
 void launch_gather_rows(const uint32_t* walks, uint64_t W, uint32_t L, const uint64_t* list, uint64_t base,
@@ -135,15 +125,15 @@ void launch_fill_u32(uint32_t* p, uint64_t cnt, uint32_t v, hipStream_t s);
 void launch_fill_u64(uint64_t* p, uint64_t cnt, uint64_t v, hipStream_t s);
 void launch_edge_hash_update(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, int insert, uint64_t* table,
                              uint64_t mask, hipStream_t s);
-void launch_edge_hash_build(const uint64_t* off, uint64_t n, const uint32_t* adj, uint64_t* table, uint64_t mask,
-                            hipStream_t s);
-void launch_filter_sizes(const uint64_t* off, uint64_t n, uint64_t* words, hipStream_t s);
-void launch_filter_pack(const uint64_t* off, uint64_t n, uint64_t* fdir, hipStream_t s);
-void launch_filter_fill(const uint64_t* off, uint64_t n, const uint32_t* adj, const uint64_t* fdir, uint32_t* pool,
+void launch_edge_hash_build(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* adj, uint64_t* table,
+                            uint64_t mask, hipStream_t s);
+void launch_filter_sizes(const uint32_t* deg, uint64_t n, uint64_t* words, hipStream_t s);
+void launch_filter_pack(const uint32_t* deg, uint64_t n, uint64_t* fdir, hipStream_t s);
+void launch_filter_fill(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* adj, const uint64_t* fdir,
+                        uint32_t* pool, hipStream_t s);
+void launch_filter_plan(const RunInfo* runs, uint64_t k, const uint32_t* deg, const uint64_t* fdir, uint64_t* need,
                         hipStream_t s);
-void launch_filter_plan(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint64_t* fdir, uint64_t* need,
-                        hipStream_t s);
-void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* adj,
+void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* deg, const uint32_t* adj,
                         const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir, uint32_t* pool,
                         hipStream_t s);
 void launch_szudzik64(int op, uint64_t cnt, uint64_t* x, uint64_t* y, uint64_t* z, hipStream_t s);

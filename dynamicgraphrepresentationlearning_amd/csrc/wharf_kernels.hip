@@ -1046,12 +1046,12 @@ __global__ void k_pairs_to_keys(const uint32_t* __restrict__ pairs, uint64_t m, 
 }
 
 // insert every (u, v) of the CSR into the edge hash set (4-key buckets, linear probing)
-__global__ void k_edge_hash_build(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ adj,
-                                  unsigned long long* __restrict__ table, uint64_t mask)
+__global__ void k_edge_hash_build(const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg, uint64_t n,
+                                  const uint32_t* __restrict__ adj, unsigned long long* __restrict__ table, uint64_t mask)
 {
     const uint64_t v0 = (uint64_t)blockIdx.x * 64;
     for (uint64_t u = v0 + threadIdx.x / 64; u < min(v0 + 64, n); u += blockDim.x / 64) {
-        const uint64_t b0 = off[u], e0 = off[u + 1];
+        const uint64_t b0 = off[u], e0 = b0 + deg[u];
         for (uint64_t j = b0 + (threadIdx.x & 63); j < e0; j += 64) {
             const unsigned long long key = (u << 32) | adj[j];
             uint64_t b = (edge_hash(key) & mask) & ~3ull;
@@ -1095,10 +1095,10 @@ void launch_edge_hash_update(const uint64_t* bkeys, uint64_t mb, const uint32_t*
                                (unsigned long long*)table, mask);
 }
 
-void launch_edge_hash_build(const uint64_t* off, uint64_t n, const uint32_t* adj, uint64_t* table, uint64_t mask,
-                            hipStream_t s)
+void launch_edge_hash_build(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* adj, uint64_t* table,
+                            uint64_t mask, hipStream_t s)
 {
-    if (n) hipLaunchKernelGGL(k_edge_hash_build, (unsigned)((n + 63) / 64), 256, 0, s, off, n, adj,
+    if (n) hipLaunchKernelGGL(k_edge_hash_build, (unsigned)((n + 63) / 64), 256, 0, s, off, deg, n, adj,
                               (unsigned long long*)table, mask);
 }
 
@@ -1107,16 +1107,16 @@ void launch_edge_hash_build(const uint64_t* off, uint64_t n, const uint32_t* adj
 // only the source rows are rebuilt (a row that outgrows its words gets new
 // ones at the end of the pool)
 // ---------------------------------------------------------------------------
-__global__ void k_filter_sizes(const uint64_t* __restrict__ off, uint64_t n, uint64_t* __restrict__ words)
+__global__ void k_filter_sizes(const uint32_t* __restrict__ deg, uint64_t n, uint64_t* __restrict__ words)
 {
     for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= n; u += (uint64_t)gridDim.x * blockDim.x)
-        words[u] = u < n ? 1ull << filt_log2_words(off[u + 1] - off[u]) : 0;
+        words[u] = u < n ? 1ull << filt_log2_words(deg[u]) : 0;
 }
 
-__global__ void k_filter_pack(const uint64_t* __restrict__ off, uint64_t n, uint64_t* __restrict__ fdir)
+__global__ void k_filter_pack(const uint32_t* __restrict__ deg, uint64_t n, uint64_t* __restrict__ fdir)
 {
     for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n; u += (uint64_t)gridDim.x * blockDim.x)
-        fdir[u] |= (uint64_t)filt_log2_words(off[u + 1] - off[u]) << kFiltOffBits;
+        fdir[u] |= (uint64_t)filt_log2_words(deg[u]) << kFiltOffBits;
 }
 
 __device__ __forceinline__ void filter_set(uint32_t* pool, uint64_t fd, uint32_t c)
@@ -1126,31 +1126,32 @@ __device__ __forceinline__ void filter_set(uint32_t* pool, uint64_t fd, uint32_t
 }
 
 // one wave per row, lanes sweep the row's targets (as k_edge_hash_build)
-__global__ void k_filter_fill(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ adj,
-                              const uint64_t* __restrict__ fdir, uint32_t* __restrict__ pool)
+__global__ void k_filter_fill(const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg, uint64_t n,
+                              const uint32_t* __restrict__ adj, const uint64_t* __restrict__ fdir,
+                              uint32_t* __restrict__ pool)
 {
     const uint64_t v0 = (uint64_t)blockIdx.x * 64;
     for (uint64_t u = v0 + threadIdx.x / 64; u < min(v0 + 64, n); u += blockDim.x / 64) {
-        const uint64_t b0 = off[u], e0 = off[u + 1], fd = fdir[u];
+        const uint64_t b0 = off[u], e0 = b0 + deg[u], fd = fdir[u];
         for (uint64_t j = b0 + (threadIdx.x & 63); j < e0; j += 64) filter_set(pool, fd, adj[j]);
     }
 }
 
 // per batch source: words its new row needs when it outgrew its old ones, else 0
-__global__ void k_filter_plan(const RunInfo* __restrict__ runs, uint64_t k, const uint64_t* __restrict__ noff,
+__global__ void k_filter_plan(const RunInfo* __restrict__ runs, uint64_t k, const uint32_t* __restrict__ deg,
                               const uint64_t* __restrict__ fdir, uint64_t* __restrict__ need)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= k; i += (uint64_t)gridDim.x * blockDim.x) {
         if (i == k) { need[i] = 0; continue; }
         const uint32_t u = runs[i].src;
-        const uint32_t lg = filt_log2_words(noff[u + 1] - noff[u]);
+        const uint32_t lg = filt_log2_words(deg[u]);
         need[i] = lg > (uint32_t)(fdir[u] >> kFiltOffBits) ? 1ull << lg : 0;
     }
 }
 
 // one block per batch source: (re)place, clear and refill its filter from the new row
 __global__ void k_filter_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ noff,
-                              const uint32_t* __restrict__ adj, const uint64_t* __restrict__ need,
+                              const uint32_t* __restrict__ deg, const uint32_t* __restrict__ adj, const uint64_t* __restrict__ need,
                               const uint64_t* __restrict__ gofs, uint64_t base, uint64_t* __restrict__ fdir,
                               uint32_t* __restrict__ pool)
 {
@@ -1158,7 +1159,7 @@ __global__ void k_filter_rows(const RunInfo* __restrict__ runs, const uint64_t* 
     const uint32_t u = runs[i].src;
     uint64_t fd = fdir[u];
     if (need[i]) {
-        const uint32_t lg = filt_log2_words(noff[u + 1] - noff[u]);
+        const uint32_t lg = filt_log2_words(deg[u]);
         fd = (base + gofs[i]) | ((uint64_t)lg << kFiltOffBits);
         __syncthreads();   // every thread has read the old descriptor
         if (threadIdx.x == 0) fdir[u] = fd;
@@ -1167,36 +1168,36 @@ __global__ void k_filter_rows(const RunInfo* __restrict__ runs, const uint64_t* 
     for (uint64_t j = threadIdx.x; j < nw; j += blockDim.x) pool[w0 + j] = 0;
     __threadfence();
     __syncthreads();
-    for (uint64_t j = noff[u] + threadIdx.x; j < noff[u + 1]; j += blockDim.x) filter_set(pool, fd, adj[j]);
+    for (uint64_t j = noff[u] + threadIdx.x; j < noff[u] + deg[u]; j += blockDim.x) filter_set(pool, fd, adj[j]);
 }
 
-void launch_filter_sizes(const uint64_t* off, uint64_t n, uint64_t* words, hipStream_t s)
+void launch_filter_sizes(const uint32_t* deg, uint64_t n, uint64_t* words, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_filter_sizes, grid_for(n + 1, 256), 256, 0, s, off, n, words);
+    hipLaunchKernelGGL(k_filter_sizes, grid_for(n + 1, 256), 256, 0, s, deg, n, words);
 }
 
-void launch_filter_pack(const uint64_t* off, uint64_t n, uint64_t* fdir, hipStream_t s)
+void launch_filter_pack(const uint32_t* deg, uint64_t n, uint64_t* fdir, hipStream_t s)
 {
-    if (n) hipLaunchKernelGGL(k_filter_pack, grid_for(n, 256), 256, 0, s, off, n, fdir);
+    if (n) hipLaunchKernelGGL(k_filter_pack, grid_for(n, 256), 256, 0, s, deg, n, fdir);
 }
 
-void launch_filter_fill(const uint64_t* off, uint64_t n, const uint32_t* adj, const uint64_t* fdir, uint32_t* pool,
+void launch_filter_fill(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* adj, const uint64_t* fdir,
+                        uint32_t* pool, hipStream_t s)
+{
+    if (n) hipLaunchKernelGGL(k_filter_fill, (unsigned)((n + 63) / 64), 256, 0, s, off, deg, n, adj, fdir, pool);
+}
+
+void launch_filter_plan(const RunInfo* runs, uint64_t k, const uint32_t* deg, const uint64_t* fdir, uint64_t* need,
                         hipStream_t s)
 {
-    if (n) hipLaunchKernelGGL(k_filter_fill, (unsigned)((n + 63) / 64), 256, 0, s, off, n, adj, fdir, pool);
+    hipLaunchKernelGGL(k_filter_plan, grid_for(k + 1, 256), 256, 0, s, runs, k, deg, fdir, need);
 }
 
-void launch_filter_plan(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint64_t* fdir, uint64_t* need,
-                        hipStream_t s)
-{
-    hipLaunchKernelGGL(k_filter_plan, grid_for(k + 1, 256), 256, 0, s, runs, k, noff, fdir, need);
-}
-
-void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* adj,
+void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* deg, const uint32_t* adj,
                         const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir, uint32_t* pool,
                         hipStream_t s)
 {
-    if (k) hipLaunchKernelGGL(k_filter_rows, (unsigned)k, 256, 0, s, runs, noff, adj, need, gofs, base, fdir, pool);
+    if (k) hipLaunchKernelGGL(k_filter_rows, (unsigned)k, 256, 0, s, runs, noff, deg, adj, need, gofs, base, fdir, pool);
 }
 
 __global__ void k_csr_to_keys(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ tgt,
@@ -1245,55 +1246,49 @@ __global__ void k_low32(const uint64_t* __restrict__ keys, uint64_t m, uint32_t*
         out[i] = (uint32_t)keys[i];
 }
 
-__global__ void k_vrec(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ row_epoch,
-                       ERec* __restrict__ vrec)
+__global__ void k_vrec(const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg, uint64_t n,
+                       const uint32_t* __restrict__ row_epoch, ERec* __restrict__ vrec)
 {
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
-        vrec[v] = make_rec((uint32_t)v, (uint32_t)(off[v + 1] - off[v]), off[v], row_epoch ? row_epoch[v] : 0u);
+        vrec[v] = make_rec((uint32_t)v, deg[v], off[v], row_epoch ? row_epoch[v] : 0u);
 }
 
-// erec[e] = vrec[adj[e]]: every CSR slot carries its target's row (rs = 2:
-// 32-B records whose anchor entry starts empty)
-__global__ void k_erec(const uint32_t* __restrict__ adj, uint64_t m, const ERec* __restrict__ vrec, ERec* __restrict__ erec,
-                       uint32_t rs)
+// erec[e] = vrec[adj[e]] for every live slot of the pool: each slot carries
+// its target's row (rs = 2: 32-B records whose anchor entry starts empty,
+// unless keep_anchors: a repack copied them along)
+__global__ void k_erec(const uint32_t* __restrict__ adj, uint64_t slots, const ERec* __restrict__ vrec,
+                       ERec* __restrict__ erec, uint32_t rs, int keep_anchors)
 {
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
-        erec[e * rs] = vrec[adj[e]];
-        if (rs == 2) reinterpret_cast<uint64_t*>(erec)[e * kAnchorStride + 2] = kAnchorNone64;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t t = adj[e];
+        if (t == kGap) continue;
+        erec[e * rs] = vrec[t];
+        if (rs == 2 && !keep_anchors) reinterpret_cast<uint64_t*>(erec)[e * kAnchorStride + 2] = kAnchorNone64;
     }
 }
 
-void launch_vrec(const uint64_t* off, uint64_t n, const uint32_t* row_epoch, ERec* vrec, hipStream_t s)
+void launch_vrec(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* row_epoch, ERec* vrec,
+                 hipStream_t s)
 {
-    if (n) hipLaunchKernelGGL(k_vrec, grid_for(n, 256), 256, 0, s, off, n, row_epoch, vrec);
+    if (n) hipLaunchKernelGGL(k_vrec, grid_for(n, 256), 256, 0, s, off, deg, n, row_epoch, vrec);
 }
 
-void launch_erec(const uint32_t* adj, uint64_t m, const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s)
+void launch_erec(const uint32_t* adj, uint64_t slots, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anchors,
+                 hipStream_t s)
 {
-    if (m) hipLaunchKernelGGL(k_erec, grid_for(m, 256), 256, 0, s, adj, m, vrec, erec, rs);
-}
-
-// anchors kept aside by an update without a second record buffer -> records
-__global__ void k_anchor_merge(const uint64_t* __restrict__ src, uint64_t m, uint64_t* __restrict__ dst)
-{
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x)
-        dst[e * kAnchorStride] = src[e];
-}
-
-void launch_anchor_merge(const uint64_t* src, uint64_t m, uint64_t* dst, hipStream_t s)
-{
-    if (m) hipLaunchKernelGGL(k_anchor_merge, grid_for(m, 256), 256, 0, s, src, m, dst);
+    if (slots) hipLaunchKernelGGL(k_erec, grid_for(slots, 256), 256, 0, s, adj, slots, vrec, erec, rs, keep_anchors);
 }
 
 // Per batch edge (sorted, unique): does it change its source row?
 //   insert: dst not yet in adj(src)  (tree_plus::uniont, wharfmh.h:511)
 //   delete: dst present in adj(src)  (tree_plus::difference, wharfmh.h:659)
 __global__ void k_batch_change(const uint64_t* __restrict__ bkeys, uint64_t mb, const uint64_t* __restrict__ off,
-                               const uint32_t* __restrict__ adj, int insert, uint32_t* __restrict__ chg)
+                               const uint32_t* __restrict__ deg, const uint32_t* __restrict__ adj, int insert,
+                               uint32_t* __restrict__ chg)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mb; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t s = (uint32_t)(bkeys[i] >> 32), d = (uint32_t)bkeys[i];
-        uint64_t lo = off[s], hi = off[s + 1];
+        uint64_t lo = off[s], hi = lo + deg[s];
         const uint64_t end = hi;
         while (lo < hi) {
             const uint64_t mid = lo + ((hi - lo) >> 1);
@@ -1313,7 +1308,8 @@ __global__ void k_run_flags(const uint64_t* __restrict__ bkeys, uint64_t mb, uin
 
 // per source run j: src, old row [off, end), batch run [rs, re)
 __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ run_start, uint64_t k,
-                           uint64_t mb, const uint64_t* __restrict__ off, RunInfo* __restrict__ runs,
+                           uint64_t mb, const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg,
+                           RunInfo* __restrict__ runs,
                            uint32_t* __restrict__ bitmap, uint32_t* __restrict__ bloom, uint32_t* __restrict__ row_epoch,
                            uint32_t epoch)
 {
@@ -1322,7 +1318,7 @@ __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* _
         const uint32_t re = j + 1 < k ? run_start[j + 1] : (uint32_t)mb;
         const uint32_t s = (uint32_t)(bkeys[rs] >> 32);
         RunInfo ri;
-        ri.src = s; ri.rs = rs; ri.re = re; ri.off = off[s]; ri.end = off[s + 1];
+        ri.src = s; ri.rs = rs; ri.re = re; ri.off = off[s]; ri.end = off[s] + deg[s];
         runs[j] = ri;
         atomicOr(bitmap + (s >> 5), 1u << (s & 31));
         const uint32_t h = bloom_hash(s), h2 = bloom_hash2(s);
@@ -1349,424 +1345,237 @@ __global__ void k_mark_sources(const uint32_t* __restrict__ src, uint64_t k, Run
     }
 }
 
-// Bucketed index over the source-run table: vtab[b] = {first run with
-// src >= b << vs, the row shift of the vertices of bucket b below it},
-// etab[b] = first run with row offset >= b << es.  A lookup reads one table
-// pair (L2-resident) and binary-searches the few runs of one bucket instead of
-// log2(k) dependent probes over the whole table; a vertex in a bucket without
-// a batch source takes its row shift straight from the table.
-__global__ void k_run_tables(const RunInfo* __restrict__ runs, uint64_t k, const uint32_t* __restrict__ cf, uint64_t mb,
-                             uint2* __restrict__ vtab, uint64_t nbv, uint32_t vs, uint32_t* __restrict__ etab,
-                             uint32_t* __restrict__ eshift, uint64_t nbe, uint32_t es)
-{
-    const uint64_t nb = nbv > nbe ? nbv : nbe;
-    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
-        if (b < nbv) {
-            const uint64_t t = b << vs;
-            uint64_t lo = 0, hi = k;
-            while (lo < hi) {
-                const uint64_t mid = lo + ((hi - lo) >> 1);
-                if (runs[mid].src < t) lo = mid + 1; else hi = mid;
-            }
-            vtab[b] = make_uint2((uint32_t)lo, cf[lo < k ? runs[lo].rs : mb]);
-        }
-        if (b < nbe) {
-            const uint64_t t = b << es;
-            uint64_t lo = 0, hi = k;
-            while (lo < hi) {
-                const uint64_t mid = lo + ((hi - lo) >> 1);
-                if (runs[mid].off < t) lo = mid + 1; else hi = mid;
-            }
-            etab[b] = (uint32_t)lo;
-            // a clean bucket: no source row starts or runs inside it, so every
-            // slot of it moves by the same shift
-            const uint64_t t2 = (b + 1) << es;
-            uint64_t lo2 = lo, hi2 = k;
-            while (lo2 < hi2) {
-                const uint64_t mid = lo2 + ((hi2 - lo2) >> 1);
-                if (runs[mid].off < t2) lo2 = mid + 1; else hi2 = mid;
-            }
-            const bool clean = lo2 == lo && (lo == 0 || runs[lo - 1].end <= t);
-            eshift[b] = clean ? 0x80000000u | (lo ? cf[runs[lo - 1].re] : 0u) : 0u;
-        }
-    }
-}
+// ---------------------------------------------------------------------------
+// Slack-row CSR: a batch touches only the rows of its sources.
+//
+// Row v lives at slots [off[v], off[v] + deg[v]) of the slot pool (adj and
+// the edge records erec share the slot index), with cap[v] >= deg[v] slots
+// reserved; unused slots hold kGap.  An update merges each source's batch
+// edges into its row in place when the row's slack holds them, else moves the
+// row to fresh slots at the end of the pool (its old slots become kGap); the
+// pool is repacked with fresh slack only when its headroom runs out.  Every
+// record caches its target's row, so the records of slots whose target is a
+// batch source (the in-edges of a changed row, whatever the graph's
+// symmetry) are rewritten by one streaming scan of the pool's targets with
+// the batch-source Bloom filter in LDS: 4 B per slot instead of moving every
+// slot's target and record (40 or 72 B) as a contiguous CSR requires.
+// ---------------------------------------------------------------------------
 
-// first run with src >= v
-__device__ __forceinline__ uint64_t run_lower_src(const RunIndex& x, uint32_t v)
-{
-    const uint64_t b = (uint64_t)v >> x.vs;
-    uint64_t lo = x.vtab[b].x, hi = x.vtab[b + 1].x;
-    while (lo < hi) {
-        const uint64_t mid = lo + ((hi - lo) >> 1);
-        if (x.runs[mid].src < v) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
-// first run whose row starts after slot e
-__device__ __forceinline__ uint64_t run_upper_off(const RunIndex& x, uint64_t e)
-{
-    const uint64_t b = e >> x.es;
-    uint64_t lo = x.etab[b], hi = x.etab[b + 1];
-    while (lo < hi) {
-        const uint64_t mid = lo + ((hi - lo) >> 1);
-        if (x.runs[mid].off <= e) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
-// new_off[v] = off[v] +/- (changing batch edges with src < v)
-__global__ void k_new_offsets(const uint64_t* __restrict__ off, uint64_t n, RunIndex x, const uint32_t* __restrict__ cf,
-                              uint64_t mb, int insert, uint64_t* __restrict__ noff)
+// from a contiguous CSR: deg, the initial capacity and the capacity as u64
+// for the layout scan (capw[n] = 0)
+__global__ void k_row_degrees(const uint64_t* __restrict__ coff, uint64_t n, uint32_t* __restrict__ deg,
+                              uint32_t* __restrict__ cap, uint64_t* __restrict__ capw, int slack)
 {
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t j = v < n ? run_lower_src(x, (uint32_t)v) : x.k;
-        const uint64_t c = cf[j < x.k ? x.runs[j].rs : mb];
-        noff[v] = insert ? off[v] + c : off[v] - c;
+        if (v == n) { capw[n] = 0; continue; }
+        const uint32_t d = (uint32_t)(coff[v + 1] - coff[v]);
+        const uint32_t c = slack ? row_cap_initial(d) : d;
+        deg[v] = d;
+        cap[v] = c;
+        capw[v] = c;
     }
 }
 
-// Move every old edge to its slot in the new CSR (one coalesced streaming pass).
-// The record of a target vertex after the batch: its row moved by the number
-// of changing batch edges with a smaller source; a batch source also changed
-// degree and had its samplers reset (epoch).  Pure arithmetic on the run
-// table, so moving the 16-B records needs no gather.
-__device__ __forceinline__ ERec patch_rec(const ERec r, const RunIndex& x, const uint32_t* __restrict__ cf, uint64_t mb,
-                                          int insert, uint32_t epoch)
+// repack: fresh capacities from the current degrees (capw as above)
+__global__ void k_row_recap(const uint32_t* __restrict__ deg, uint64_t n, uint32_t* __restrict__ cap,
+                            uint64_t* __restrict__ capw, int slack)
 {
-    const uint32_t v = r.v;
-    const uint64_t b = (uint64_t)v >> x.vs;
-    const uint2 t0 = x.vtab[b], t1 = x.vtab[b + 1];
-    uint64_t off = r.oe & kOffMask;
-    uint32_t ep = (uint32_t)(r.oe >> kOffBits), deg = r.deg;
-    if (t0.x == t1.x) {   // no batch source in v's bucket (the common case)
-        off = insert ? off + t0.y : off - t0.y;
-        return make_rec(v, deg, off, ep);
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (uint64_t)gridDim.x * blockDim.x) {
+        if (v == n) { capw[n] = 0; continue; }
+        const uint32_t c = slack ? row_cap_initial(deg[v]) : deg[v];
+        cap[v] = c;
+        capw[v] = c;
     }
-    const RunInfo* __restrict__ runs = x.runs;
-    const uint64_t k = x.k;
-    uint64_t lo = t0.x, hi = t1.x;
-    while (lo < hi) {
-        const uint64_t mid = lo + ((hi - lo) >> 1);
-        if (runs[mid].src < v) lo = mid + 1; else hi = mid;
-    }
-    const uint64_t shift = lo < k ? cf[runs[lo].rs] : cf[mb];
-    off = insert ? off + shift : off - shift;
-    if (lo < k && runs[lo].src == v) {
-        const uint32_t d = cf[runs[lo].re] - cf[runs[lo].rs];
-        deg = insert ? deg + d : deg - d;
-        ep = epoch;
-    }
-    return make_rec(v, deg, off, ep);
 }
 
-// The source ids and their row shifts in LDS (k + 1 entries each, ~0 sentinel).
-__device__ __forceinline__ void run_table_to_lds(const RunIndex& rx, const uint32_t* __restrict__ cf, uint64_t mb,
-                                                 uint32_t* s_tab)
+// deg as u64 with a trailing 0 (the scan of a compacted export)
+__global__ void k_deg_u64(const uint32_t* __restrict__ deg, uint64_t n, uint64_t* __restrict__ out)
 {
-    const uint32_t k = (uint32_t)rx.k;
-    for (uint32_t j = threadIdx.x; j <= k; j += blockDim.x) {
-        s_tab[j] = j < k ? rx.runs[j].src : ~0u;
-        s_tab[k + 1 + j] = cf[j < k ? rx.runs[j].rs : mb];
-    }
-    __syncthreads();
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (uint64_t)gridDim.x * blockDim.x)
+        out[v] = v < n ? deg[v] : 0;
 }
 
-// patch_rec with the source search in LDS
-__device__ __forceinline__ ERec patch_rec_lds(const ERec r, const RunIndex& rx, const uint32_t* s_tab,
-                                              const uint32_t* __restrict__ cf, int insert, uint32_t epoch)
+// dst[doff[v] + i] = src[soff[v] + i] for i < deg[v], one wave per row; with
+// sanc, the 8-B anchor entries travel along (stride kAnchorStride)
+__global__ void k_copy_rows(const uint64_t* __restrict__ soff, const uint32_t* __restrict__ deg,
+                            const uint32_t* __restrict__ src, const uint64_t* __restrict__ doff, uint64_t n,
+                            uint32_t* __restrict__ dst, const uint64_t* __restrict__ sanc, uint64_t* __restrict__ danc)
 {
-    const uint32_t k = (uint32_t)rx.k;
-    uint32_t lo = 0, hi = k;
+    const uint64_t v0 = (uint64_t)blockIdx.x * 64;
+    for (uint64_t v = v0 + threadIdx.x / 64; v < min(v0 + 64, n); v += blockDim.x / 64) {
+        const uint64_t b = soff[v], o = doff[v];
+        const uint32_t d = deg[v];
+        for (uint32_t j = threadIdx.x & 63; j < d; j += 64) {
+            dst[o + j] = src[b + j];
+            if (sanc) danc[(o + j) * kAnchorStride] = sanc[(b + j) * kAnchorStride];
+        }
+    }
+}
+
+// per run: the source's new degree and, when it outgrows the row's slots,
+// the capacity of its new place (need), and its old degree (save: the
+// scratch copy the merge reads)
+__global__ void k_plan_rows(const RunInfo* __restrict__ runs, uint64_t k, const uint32_t* __restrict__ cap,
+                            const uint32_t* __restrict__ cf, int insert, int slack, uint64_t* __restrict__ need,
+                            uint64_t* __restrict__ save, RowPlan* __restrict__ plan)
+{
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= k; j += (uint64_t)gridDim.x * blockDim.x) {
+        if (j == k) { need[k] = 0; save[k] = 0; continue; }
+        const RunInfo ri = runs[j];
+        const uint32_t d = (uint32_t)(ri.end - ri.off), c = cap[ri.src];
+        const uint32_t delta = cf[ri.re] - cf[ri.rs];
+        const uint32_t nd = insert ? d + delta : d - delta;
+        const bool reloc = nd > c;
+        const uint32_t nc = reloc ? (slack ? row_cap_grown(nd) : nd) : c;
+        need[j] = reloc ? nc : 0;
+        save[j] = d;
+        plan[j] = RowPlan{reloc ? kRelocate : ri.off, nd, nc, c};
+    }
+}
+
+// block per run: the old row, copied aside (the merge may overwrite it in place)
+__global__ void k_save_rows(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ adj,
+                            const uint64_t* __restrict__ sofs, uint32_t* __restrict__ scratch)
+{
+    const RunInfo ri = runs[blockIdx.x];
+    uint32_t* __restrict__ out = scratch + sofs[blockIdx.x];
+    for (uint64_t i = threadIdx.x; i < ri.end - ri.off; i += blockDim.x) out[i] = adj[ri.off + i];
+}
+
+// first index in a[0, n) with a[i] >= x (ascending u32)
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* __restrict__ a, uint32_t n, uint32_t x)
+{
+    uint32_t lo = 0, hi = n;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (s_tab[mid] < r.v) lo = mid + 1; else hi = mid;
+        if (a[mid] < x) lo = mid + 1; else hi = mid;
     }
-    const uint64_t shift = s_tab[k + 1 + lo];
-    uint64_t off = r.oe & kOffMask;
-    uint32_t ep = (uint32_t)(r.oe >> kOffBits), deg = r.deg;
-    off = insert ? off + shift : off - shift;
-    if (s_tab[lo] == r.v) {   // a batch source (rare): degree change, sampler reset
-        const uint32_t d = cf[rx.runs[lo].re] - cf[rx.runs[lo].rs];
-        deg = insert ? deg + d : deg - d;
-        ep = epoch;
+    return lo;
+}
+// the same over the low words of sorted (src, dst) keys
+__device__ __forceinline__ uint32_t lower_bound_dst(const uint64_t* __restrict__ k, uint32_t n, uint32_t x)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((uint32_t)k[mid] < x) lo = mid + 1; else hi = mid;
     }
-    return make_rec(r.v, deg, off, ep);
+    return lo;
 }
 
-// LDS = true (up to 10 k source runs, 80 KiB): the source ids and their row
-// shifts sit in LDS, so the target-record patch is a binary search in LDS
-// instead of a random L2 lookup per edge (random lookups, even L2 hits, cap
-// the kernel at the chip's random-access rate, ~45 G/s: 1.9 ms for
-// configs[2]'s 86 M edges).
-// Records have stride rs (1: 16 B, 2: 32 B with the anchor entry); anchors
-// are read with stride as_in and written with stride as_out (inside the
-// records, or to a plain array when the records are rebuilt afterwards).
-template <bool LDS>
-__global__ __launch_bounds__(LDS ? 1024 : 256) void k_move_edges(const uint32_t* __restrict__ adj, const uint64_t* __restrict__ anc,
-                             uint32_t as_in, uint64_t m, RunIndex rx, const uint64_t* __restrict__ bkeys,
-                             const uint32_t* __restrict__ cf, const uint64_t* __restrict__ noff, int insert,
-                             uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc, uint32_t as_out, uint64_t cap,
-                             const ERec* __restrict__ oerec, ERec* __restrict__ nerec, uint32_t rs, uint64_t mb,
-                             uint32_t epoch)
+// Block per run: write the source's new row, ascending (tree_plus::uniont /
+// difference, wharfmh.h:511,659).  Insert: old element i lands at i + (new
+// batch edges below it), new edge t at (new edges before t) + (old elements
+// below it).  Delete: old element i, unless deleted, lands at i - (deleted
+// edges below it).  Slots left over become kGap: the tail of a shrunk row,
+// or the whole old place of a moved row and the slack of its new one.
+__global__ void k_merge_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ bkeys,
+                             const uint32_t* __restrict__ chg, const uint32_t* __restrict__ cf,
+                             const uint32_t* __restrict__ scratch, const uint64_t* __restrict__ sofs,
+                             const uint64_t* __restrict__ relofs, uint64_t pool_end, int insert,
+                             RowPlan* __restrict__ plan, uint32_t* __restrict__ adj)
 {
-    const RunInfo* __restrict__ runs = rx.runs;
-    extern __shared__ uint32_t s_tab[];   // LDS: src[k + 1] (sentinel ~0), shift[k + 1]
-    if constexpr (LDS) run_table_to_lds(rx, cf, mb, s_tab);
-    auto patch = [&](const ERec r) -> ERec {
-        if constexpr (!LDS) return patch_rec(r, rx, cf, mb, insert, epoch);
-        else return patch_rec_lds(r, rx, s_tab, cf, insert, epoch);
-    };
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t x = adj[e];
-        const uint32_t es = rx.eshift[e >> rx.es];
-        if (es >> 31) {   // clean bucket: shift from the table, no run search
-            const uint64_t shift = es & 0x7FFFFFFFu;
-            const uint64_t np = insert ? e + shift : e - shift;
-            if (np >= cap) continue;
-            nadj[np] = x;
-            if (nanc) nanc[np * as_out] = anc[e * as_in];
-            if (nerec) nerec[np * rs] = patch(oerec[e * rs]);
-            continue;
-        }
-        // last source run whose row starts at or before e
-        const uint64_t lo = run_upper_off(rx, e);
-        if (lo == 0) {
-            nadj[e] = x;
-            if (nanc) nanc[e * as_out] = anc[e * as_in];
-            if (nerec) nerec[e * rs] = patch(oerec[e * rs]);
-            continue;
-        }
-        const RunInfo ri = runs[lo - 1];
-        if (e < ri.end) {
-            // inside a source row: position = new row start + rank among survivors
-            uint64_t b = ri.rs, t = ri.re;
-            while (b < t) {
-                const uint64_t mid = b + ((t - b) >> 1);
-                if ((uint32_t)bkeys[mid] < x) b = mid + 1; else t = mid;
-            }
-            const uint64_t before = cf[b] - cf[ri.rs];
-            if (!insert && b < ri.re && (uint32_t)bkeys[b] == x) continue;   // deleted
-            const uint64_t np = noff[ri.src] + (e - ri.off) + (insert ? before : -(int64_t)before);
-            if (np >= cap) continue;   // never taken for a consistent CSR; keeps a bad input in bounds
-            nadj[np] = x;
-            if (nanc) nanc[np * as_out] = kAnchorNone64;
-        } else {
-            const uint64_t shift = cf[ri.re];
-            const uint64_t np = insert ? e + shift : e - shift;
-            if (np >= cap) continue;
-            nadj[np] = x;
-            if (nanc) nanc[np * as_out] = anc[e * as_in];
-            if (nerec) nerec[np * rs] = patch(oerec[e * rs]);
+    const uint64_t j = blockIdx.x;
+    const RunInfo ri = runs[j];
+    const RowPlan p = plan[j];
+    const bool reloc = p.noff == kRelocate;
+    const uint64_t noff = reloc ? pool_end + relofs[j] : ri.off;
+    const uint32_t d = (uint32_t)(ri.end - ri.off), nb = ri.re - ri.rs, base = cf[ri.rs];
+    const uint32_t* __restrict__ old = scratch + sofs[j];
+    const uint64_t* __restrict__ bk = bkeys + ri.rs;
+    for (uint32_t i = threadIdx.x; i < d; i += blockDim.x) {
+        const uint32_t x = old[i];
+        const uint32_t lb = lower_bound_dst(bk, nb, x);
+        const uint32_t below = cf[ri.rs + lb] - base;
+        if (insert) {
+            adj[noff + i + below] = x;
+        } else if (!(lb < nb && (uint32_t)bk[lb] == x && chg[ri.rs + lb])) {
+            adj[noff + i - below] = x;
         }
     }
-}
-
-// ---------------------------------------------------------------------------
-// In-place record move, for graphs whose second record buffer does not fit
-// (configs[4]: 3.6 G slots x 32 B = 115 GB).  Every old slot e outside the
-// batch sources' rows moves to e + sh(e) (insert) or e - sh(e) (delete), sh
-// non-decreasing in e and at most S = the batch's changed edges; the rows of
-// batch sources are rebuilt afterwards (k_erec_rows).  The records are cut in
-// chunks of C >= S slots, one workgroup per chunk:
-//   * insert: a chunk's records land in the chunk itself or in the first S
-//     slots (the head) of the next chunk.  k_save_edges copies every head
-//     aside first; each workgroup then sweeps its chunk from the top down in
-//     tiles (read the tile - its head from the copy - barrier, write), so a
-//     slot is never overwritten before it is read.
-//   * delete: the mirror image (tails saved, tiles bottom up).
-// Destinations are distinct (the move is the CSR's slot permutation), so the
-// only hazard is read-after-overwrite, which the saved heads / tails and the
-// sweep direction exclude.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t moved_slot(const RunIndex& rx, const uint32_t* __restrict__ cf, int insert, uint64_t e)
-{
-    const uint32_t es = rx.eshift[e >> rx.es];
-    if (es >> 31) {
-        const uint64_t sh = es & 0x7FFFFFFFu;
-        return insert ? e + sh : e - sh;
-    }
-    const uint64_t lo = run_upper_off(rx, e);
-    if (lo == 0) return e;
-    const RunInfo ri = rx.runs[lo - 1];
-    if (e < ri.end) return ~0ull;   // in a source row: rebuilt
-    const uint64_t sh = cf[ri.re];
-    return insert ? e + sh : e - sh;
-}
-
-__device__ __forceinline__ void copy_rec(const ERec* __restrict__ src, ERec* __restrict__ dst, uint32_t rs)
-{
-    const uint4* s4 = reinterpret_cast<const uint4*>(src);
-    uint4* d4 = reinterpret_cast<uint4*>(dst);
-    d4[0] = s4[0];
-    if (rs == 2) d4[1] = s4[1];
-}
-
-// the slots of chunk c that the neighbouring chunk writes into: head [lo, lo + S)
-// for inserts (c > 0), tail [hi - S, hi) for deletes (c < last)
-__device__ __forceinline__ bool saved_region(uint64_t c, uint64_t nchunks, uint64_t C, uint64_t S, uint64_t m,
-                                             int insert, uint64_t& b0)
-{
-    const uint64_t lo = c * C, hi = lo + C < m ? lo + C : m;
     if (insert) {
-        b0 = lo;
-        return c > 0 && S > 0;
-    }
-    b0 = hi > S ? hi - S : 0;
-    return c + 1 < nchunks && S > 0;
-}
-
-__global__ void k_save_edges(const ERec* __restrict__ rec, uint32_t rs, uint64_t m, uint64_t C, uint64_t S, int insert,
-                             ERec* __restrict__ save)
-{
-    const uint64_t nchunks = (m + C - 1) / C;
-    const uint64_t total = nchunks * S;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t c = i / S, j = i - c * S;
-        uint64_t b0;
-        if (!saved_region(c, nchunks, C, S, m, insert, b0)) continue;
-        if (b0 + j < m) copy_rec(rec + (b0 + j) * rs, save + i * rs, rs);
-    }
-}
-
-// each thread moves kInplaceR records per tile (independent loads in flight)
-constexpr uint32_t kInplaceR = 4;
-
-template <bool INSERT, bool LDS>
-__global__ __launch_bounds__(1024) void k_move_records_inplace(ERec* __restrict__ rec, uint32_t rs, uint64_t m,
-                                                               uint64_t C, uint64_t S, const ERec* __restrict__ save,
-                                                               RunIndex rx, const uint32_t* __restrict__ cf,
-                                                               uint64_t mb, uint32_t epoch)
-{
-    extern __shared__ uint32_t s_tab[];
-    if constexpr (LDS) run_table_to_lds(rx, cf, mb, s_tab);
-    const uint64_t nchunks = (m + C - 1) / C;
-    const uint64_t c = blockIdx.x;
-    const uint64_t lo = c * C, hi = lo + C < m ? lo + C : m;
-    uint64_t b0;
-    const bool has_saved = saved_region(c, nchunks, C, S, m, INSERT, b0);
-    const uint64_t tsz = (uint64_t)blockDim.x * kInplaceR;
-    const uint64_t ntile = (hi - lo + tsz - 1) / tsz;
-    for (uint64_t t = 0; t < ntile; t++) {
-        const uint64_t tile = INSERT ? ntile - 1 - t : t;
-        uint64_t np[kInplaceR];
-        uint4 q0[kInplaceR], q1[kInplaceR];
-#pragma unroll
-        for (uint32_t k = 0; k < kInplaceR; k++) {
-            const uint64_t e = lo + tile * tsz + k * blockDim.x + threadIdx.x;
-            np[k] = ~0ull;
-            q0[k] = q1[k] = make_uint4(0, 0, 0, 0);
-            if (e < hi) {
-                np[k] = moved_slot(rx, cf, INSERT, e);
-                if (np[k] != ~0ull) {
-                    const bool from_save = has_saved && e >= b0 && e < b0 + S;
-                    const uint4* src =
-                        reinterpret_cast<const uint4*>(from_save ? save + (c * S + (e - b0)) * rs : rec + e * rs);
-                    q0[k] = src[0];
-                    if (rs == 2) q1[k] = src[1];
-                }
-            }
-        }
-        __syncthreads();   // every read of this tile before any write
-#pragma unroll
-        for (uint32_t k = 0; k < kInplaceR; k++) {
-            if (np[k] == ~0ull) continue;
-            ERec r;
-            r.v = q0[k].x;
-            r.deg = q0[k].y;
-            r.oe = ((uint64_t)q0[k].w << 32) | q0[k].z;
-            const ERec pr = LDS ? patch_rec_lds(r, rx, s_tab, cf, INSERT, epoch) : patch_rec(r, rx, cf, mb, INSERT, epoch);
-            uint4* dst = reinterpret_cast<uint4*>(rec + np[k] * rs);
-            dst[0] = make_uint4(pr.v, pr.deg, (uint32_t)pr.oe, (uint32_t)(pr.oe >> 32));
-            if (rs == 2) dst[1] = q1[k];   // the anchor entry travels with its slot
+        for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x) {
+            if (!chg[ri.rs + t]) continue;
+            const uint32_t x = (uint32_t)bk[t];
+            adj[noff + (cf[ri.rs + t] - base) + lower_bound_u32(old, d, x)] = x;
         }
     }
-}
-
-uint64_t inplace_chunk(uint64_t S) { return std::max<uint64_t>(1ull << 20, S); }
-
-// bytes of LDS a 1024-thread record-move workgroup may hold its source table in
-// (two workgroups per CU; 0 with WHARF_MOVE_NO_LDS=1, for tests)
-uint64_t move_lds_limit()
-{
-    static int max_lds = -1;
-    if (max_lds < 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) max_lds = 65536;
-        max_lds = std::min(max_lds, 80 * 1024);
-    }
-    const char* no_lds = getenv("WHARF_MOVE_NO_LDS");
-    return (no_lds && *no_lds == '1') ? 0 : (uint64_t)max_lds;
-}
-
-void launch_move_records_inplace(ERec* rec, uint32_t rs, uint64_t m, uint64_t S, ERec* save, const RunIndex& x,
-                                 const uint32_t* cf, uint64_t mb, int insert, uint32_t epoch, hipStream_t s)
-{
-    if (!m) return;
-    const uint64_t C = inplace_chunk(S);
-    const uint64_t nchunks = (m + C - 1) / C;
-    if (S) hipLaunchKernelGGL(k_save_edges, grid_for(nchunks * S, 256), 256, 0, s, rec, rs, m, C, S, insert, save);
-    const size_t lds = (size_t)(x.k + 1) * 8;
-    const bool in_lds = lds <= move_lds_limit();
-#define WHARF_INPLACE(I, D) \
-    hipLaunchKernelGGL((k_move_records_inplace<I, D>), (unsigned)nchunks, 1024, D ? lds : 0, s, rec, rs, m, C, S, save, x, cf, mb, epoch)
-    if (insert) {
-        if (in_lds) WHARF_INPLACE(true, true); else WHARF_INPLACE(true, false);
+    if (reloc) {
+        for (uint32_t i = threadIdx.x; i < p.ocap; i += blockDim.x) adj[ri.off + i] = kGap;
+        for (uint32_t i = p.ndeg + threadIdx.x; i < p.ncap; i += blockDim.x) adj[noff + i] = kGap;
     } else {
-        if (in_lds) WHARF_INPLACE(false, true); else WHARF_INPLACE(false, false);
+        for (uint32_t i = p.ndeg + threadIdx.x; i < d; i += blockDim.x) adj[ri.off + i] = kGap;
     }
-#undef WHARF_INPLACE
+    __syncthreads();   // every thread has read plan[j] before it is resolved
+    if (threadIdx.x == 0) plan[j].noff = noff;
+}
+
+// per run: the source's new row and record (its epoch was set by k_run_info)
+__global__ void k_commit_rows(const RunInfo* __restrict__ runs, uint64_t k, const RowPlan* __restrict__ plan,
+                              uint32_t epoch, uint64_t* __restrict__ off, uint32_t* __restrict__ deg,
+                              uint32_t* __restrict__ cap, ERec* __restrict__ vrec)
+{
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = runs[j].src;
+        const RowPlan p = plan[j];
+        off[s] = p.noff;
+        deg[s] = p.ndeg;
+        cap[s] = p.ncap;
+        vrec[s] = make_rec(s, p.ndeg, p.noff, epoch);
+    }
 }
 
 // records of the rebuilt source rows: erec[slot] = vrec[adj[slot]] (block per
 // run); their anchor entries (states (target, source), whose anchors read the
 // source's row) start empty: see anchor_lookup and DESIGN.md §4
-__global__ void k_erec_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ noff,
-                            const uint32_t* __restrict__ nadj, const ERec* __restrict__ vrec, ERec* __restrict__ erec,
-                            uint32_t rs)
+__global__ void k_erec_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ off,
+                            const uint32_t* __restrict__ deg, const uint32_t* __restrict__ adj,
+                            const ERec* __restrict__ vrec, ERec* __restrict__ erec, uint32_t rs)
 {
     const uint32_t s = runs[blockIdx.x].src;
-    const uint64_t b = noff[s], e = noff[s + 1];
+    const uint64_t b = off[s], e = b + deg[s];
     for (uint64_t j = b + threadIdx.x; j < e; j += blockDim.x) {
-        erec[j * rs] = vrec[nadj[j]];
+        erec[j * rs] = vrec[adj[j]];
         if (rs == 2) reinterpret_cast<uint64_t*>(erec)[j * kAnchorStride + 2] = kAnchorNone64;
     }
 }
 
-void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* nadj, const ERec* vrec,
-                      ERec* erec, uint32_t rs, hipStream_t s)
+// In-edge records of the batch sources: every slot whose target is a source
+// gets the source's new row record (the anchor entry stays: its epoch tag is
+// checked against the new row epoch, anchor_lookup).  One streaming pass over
+// the pool's targets, four slots per 16-B load; the Bloom filter of the
+// sources sits in LDS and only its positives read the exact bitmap.
+__device__ __forceinline__ void patch_slot(uint32_t t, uint64_t e, const uint32_t* s_bloom, const uint32_t* bitmap,
+                                           const ERec* vrec, ERec* erec, uint32_t rs)
 {
-    if (k) hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, noff, nadj, vrec, erec, rs);
+    if (t == kGap) return;
+    const uint32_t h = bloom_hash(t), h2 = bloom_hash2(t);
+    if (!((s_bloom[h >> 5] >> (h & 31)) & (s_bloom[h2 >> 5] >> (h2 & 31)) & 1u)) return;
+    if (!((bitmap[t >> 5] >> (t & 31)) & 1u)) return;
+    erec[e * rs] = vrec[t];
 }
 
-// Place the inserted edges (insert only).
-__global__ void k_place_new(const uint64_t* __restrict__ bkeys, uint64_t mb, const uint32_t* __restrict__ chg,
-                            const uint32_t* __restrict__ cf, const uint32_t* __restrict__ run_start, uint64_t k,
-                            const RunInfo* __restrict__ runs, const uint32_t* __restrict__ adj,
-                            const uint64_t* __restrict__ noff, uint32_t* __restrict__ nadj, uint64_t* __restrict__ nanc,
-                            uint32_t as_out, uint64_t cap)
+__global__ __launch_bounds__(256) void k_patch_in_edges(const uint32_t* __restrict__ adj, uint64_t slots,
+                                                       const uint32_t* __restrict__ bitmap,
+                                                       const uint32_t* __restrict__ bloom,
+                                                       const ERec* __restrict__ vrec, ERec* __restrict__ erec,
+                                                       uint32_t rs)
 {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mb; i += (uint64_t)gridDim.x * blockDim.x) {
-        if (!chg[i]) continue;
-        uint64_t lo = 0, hi = k;
-        while (lo < hi) {
-            const uint64_t mid = lo + ((hi - lo) >> 1);
-            if (run_start[mid] <= i) lo = mid + 1; else hi = mid;
-        }
-        const RunInfo ri = runs[lo - 1];
-        const uint32_t d = (uint32_t)bkeys[i];
-        uint64_t b = ri.off, t = ri.end;
-        while (b < t) {
-            const uint64_t mid = b + ((t - b) >> 1);
-            if (adj[mid] < d) b = mid + 1; else t = mid;
-        }
-        const uint64_t np = noff[ri.src] + (cf[i] - cf[ri.rs]) + (b - ri.off);
-        if (np >= cap) continue;
-        nadj[np] = d;
-        if (nanc) nanc[np * as_out] = kAnchorNone64;
+    __shared__ uint32_t s_bloom[kBloomWords];
+    for (uint32_t i = threadIdx.x; i < kBloomWords; i += blockDim.x) s_bloom[i] = bloom[i];
+    __syncthreads();
+    const uint64_t n4 = slots / 4, stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* __restrict__ a4 = reinterpret_cast<const u32x4*>(adj);
+    for (uint64_t q = g; q < n4; q += stride) {
+        const u32x4 t = __builtin_nontemporal_load(a4 + q);
+        patch_slot(t.x, 4 * q, s_bloom, bitmap, vrec, erec, rs);
+        patch_slot(t.y, 4 * q + 1, s_bloom, bitmap, vrec, erec, rs);
+        patch_slot(t.z, 4 * q + 2, s_bloom, bitmap, vrec, erec, rs);
+        patch_slot(t.w, 4 * q + 3, s_bloom, bitmap, vrec, erec, rs);
     }
+    if (g < slots - 4 * n4) patch_slot(adj[4 * n4 + g], 4 * n4 + g, s_bloom, bitmap, vrec, erec, rs);
 }
 
 // ---------------------------------------------------------------------------
@@ -2011,57 +1820,56 @@ void launch_offsets_from_keys(const uint64_t* keys, uint64_t m, uint64_t n, uint
 { hipLaunchKernelGGL(k_offsets_from_keys, grid_for(n + 1, 256), 256, 0, s, keys, m, n, off); }
 void launch_low32(const uint64_t* keys, uint64_t m, uint32_t* out, hipStream_t s)
 { hipLaunchKernelGGL(k_low32, grid_for(m, 256), 256, 0, s, keys, m, out); }
-void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off, const uint32_t* adj, int insert, uint32_t* chg, hipStream_t s)
-{ hipLaunchKernelGGL(k_batch_change, grid_for(mb, 256), 256, 0, s, bkeys, mb, off, adj, insert, chg); }
+void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off, const uint32_t* deg, const uint32_t* adj,
+                         int insert, uint32_t* chg, hipStream_t s)
+{ hipLaunchKernelGGL(k_batch_change, grid_for(mb, 256), 256, 0, s, bkeys, mb, off, deg, adj, insert, chg); }
 void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_t s)
 { hipLaunchKernelGGL(k_run_flags, grid_for(mb, 256), 256, 0, s, bkeys, mb, f); }
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
-                     RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, uint32_t* row_epoch, uint32_t epoch,
-                     hipStream_t s)
-{ hipLaunchKernelGGL(k_run_info, grid_for(k, 256), 256, 0, s, bkeys, run_start, k, mb, off, runs, bitmap, bloom, row_epoch, epoch); }
+                     const uint32_t* deg, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, uint32_t* row_epoch,
+                     uint32_t epoch, hipStream_t s)
+{ hipLaunchKernelGGL(k_run_info, grid_for(k, 256), 256, 0, s, bkeys, run_start, k, mb, off, deg, runs, bitmap, bloom, row_epoch, epoch); }
 
 void launch_mark_sources(const uint32_t* src, uint64_t k, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, hipStream_t s)
 {
     if (k) hipLaunchKernelGGL(k_mark_sources, grid_for(k, 256), 256, 0, s, src, k, runs, bitmap, bloom);
 }
-void launch_run_tables(const RunInfo* runs, uint64_t k, const uint32_t* cf, uint64_t mb, uint64_t n, uint64_t m,
-                       uint32_t* tabs, RunIndex* x, hipStream_t s)
+void launch_row_degrees(const uint64_t* coff, uint64_t n, uint32_t* deg, uint32_t* cap, uint64_t* capw, int slack,
+                        hipStream_t s)
+{ hipLaunchKernelGGL(k_row_degrees, grid_for(n + 1, 256), 256, 0, s, coff, n, deg, cap, capw, slack); }
+void launch_row_recap(const uint32_t* deg, uint64_t n, uint32_t* cap, uint64_t* capw, int slack, hipStream_t s)
+{ hipLaunchKernelGGL(k_row_recap, grid_for(n + 1, 256), 256, 0, s, deg, n, cap, capw, slack); }
+void launch_deg_u64(const uint32_t* deg, uint64_t n, uint64_t* out, hipStream_t s)
+{ hipLaunchKernelGGL(k_deg_u64, grid_for(n + 1, 256), 256, 0, s, deg, n, out); }
+void launch_copy_rows(const uint64_t* soff, const uint32_t* deg, const uint32_t* src, const uint64_t* doff, uint64_t n,
+                      uint32_t* dst, const uint64_t* sanc, uint64_t* danc, hipStream_t s)
+{ if (n) hipLaunchKernelGGL(k_copy_rows, (unsigned)((n + 63) / 64), 256, 0, s, soff, deg, src, doff, n, dst, sanc, danc); }
+void launch_plan_rows(const RunInfo* runs, uint64_t k, const uint32_t* cap, const uint32_t* cf, int insert, int slack,
+                      uint64_t* need, uint64_t* save, RowPlan* plan, hipStream_t s)
+{ hipLaunchKernelGGL(k_plan_rows, grid_for(k + 1, 256), 256, 0, s, runs, k, cap, cf, insert, slack, need, save, plan); }
+void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* adj, const uint64_t* sofs, uint32_t* scratch,
+                      hipStream_t s)
+{ if (k) hipLaunchKernelGGL(k_save_rows, (unsigned)k, 256, 0, s, runs, adj, sofs, scratch); }
+void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint64_t* bkeys, const uint32_t* chg, const uint32_t* cf,
+                       const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs, uint64_t pool_end,
+                       int insert, RowPlan* plan, uint32_t* adj, hipStream_t s)
 {
-    x->runs = runs;
-    x->k = k;
-    x->vs = run_table_shift(n, 18);
-    x->es = run_table_shift(m, 20);
-    const uint64_t nbv = (n >> x->vs) + 2, nbe = (m >> x->es) + 2;
-    uint2* vt = reinterpret_cast<uint2*>(tabs);
-    x->vtab = vt;
-    x->etab = tabs + 2 * nbv;
-    x->eshift = tabs + 2 * nbv + nbe;
-    hipLaunchKernelGGL(k_run_tables, grid_for(std::max(nbv, nbe), 256), 256, 0, s, runs, k, cf, mb, vt, nbv, x->vs,
-                       tabs + 2 * nbv, tabs + 2 * nbv + nbe, nbe, x->es);
+    if (k) hipLaunchKernelGGL(k_merge_rows, (unsigned)k, 256, 0, s, runs, bkeys, chg, cf, scratch, sofs, relofs,
+                              pool_end, insert, plan, adj);
 }
-void launch_new_offsets(const uint64_t* off, uint64_t n, const RunIndex& x, const uint32_t* cf, uint64_t mb, int insert,
-                        uint64_t* noff, hipStream_t s)
-{ hipLaunchKernelGGL(k_new_offsets, grid_for(n + 1, 256), 256, 0, s, off, n, x, cf, mb, insert, noff); }
-void launch_move_edges(const uint32_t* adj, const uint64_t* anc, uint32_t as_in, uint64_t m, const RunIndex& x,
-                       const uint64_t* bkeys, const uint32_t* cf, const uint64_t* noff, int insert, uint32_t* nadj,
-                       uint64_t* nanc, uint32_t as_out, uint64_t cap, const ERec* oerec, ERec* nerec, uint32_t rs,
-                       uint64_t mb, uint32_t epoch, hipStream_t s)
+void launch_commit_rows(const RunInfo* runs, uint64_t k, const RowPlan* plan, uint32_t epoch, uint64_t* off,
+                        uint32_t* deg, uint32_t* cap, ERec* vrec, hipStream_t s)
+{ if (k) hipLaunchKernelGGL(k_commit_rows, grid_for(k, 256), 256, 0, s, runs, k, plan, epoch, off, deg, cap, vrec); }
+void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* off, const uint32_t* deg, const uint32_t* adj,
+                      const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s)
+{ if (k) hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, off, deg, adj, vrec, erec, rs); }
+void launch_patch_in_edges(const uint32_t* adj, uint64_t slots, const uint32_t* bitmap, const uint32_t* bloom,
+                           const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s)
 {
-    if (!m) return;
-    if ((x.k + 1) * 8 <= move_lds_limit()) {
-        const size_t lds = (size_t)(x.k + 1) * 8;
-        const unsigned grid = (unsigned)std::min<uint64_t>((m + 1023) / 1024, (uint64_t)cu_count() * 2);
-        hipLaunchKernelGGL(k_move_edges<true>, grid, 1024, lds, s, adj, anc, as_in, m, x, bkeys, cf, noff, insert, nadj,
-                           nanc, as_out, cap, oerec, nerec, rs, mb, epoch);
-    } else {
-        hipLaunchKernelGGL(k_move_edges<false>, grid_for(m, 256), 256, 0, s, adj, anc, as_in, m, x, bkeys, cf, noff,
-                           insert, nadj, nanc, as_out, cap, oerec, nerec, rs, mb, epoch);
-    }
+    if (!slots) return;
+    const unsigned grid = (unsigned)std::min<uint64_t>((slots / 4 + 255) / 256 + 1, (uint64_t)cu_count() * 8);
+    hipLaunchKernelGGL(k_patch_in_edges, grid, 256, 0, s, adj, slots, bitmap, bloom, vrec, erec, rs);
 }
-void launch_place_new(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint32_t* cf, const uint32_t* run_start,
-                      uint64_t k, const RunInfo* runs, const uint32_t* adj, const uint64_t* noff, uint32_t* nadj,
-                      uint64_t* nanc, uint32_t as_out, uint64_t cap, hipStream_t s)
-{ hipLaunchKernelGGL(k_place_new, grid_for(mb, 256), 256, 0, s, bkeys, mb, chg, cf, run_start, k, runs, adj, noff, nadj, nanc, as_out, cap); }
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s)
 {
     if (!W) return;

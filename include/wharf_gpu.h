@@ -78,8 +78,14 @@ typedef struct wharf_stats {
     double   last_total_ms;        /* host wall time of the last call */
     uint64_t hbm_bytes_walks;      /* resident bytes: walk matrix */
     uint64_t hbm_bytes_graph;      /* resident bytes: CSR + vertex records (+ anchors) */
-    double   last_csr_move_ms;     /* device time of the last update's streaming CSR pass (k_move_edges) */
-    uint64_t last_moved_slots;     /* old CSR slots that pass read (the old m) */
+    double   last_csr_move_ms;     /* device time of the last update's streaming pass over the slot pool
+                                      (k_patch_in_edges: the in-edge records of the batch sources) */
+    uint64_t last_moved_slots;     /* pool slots that pass read */
+    /* slack-row CSR: row v = slots [off, off + deg) of a pool with cap >= deg reserved */
+    uint64_t pool_slots;           /* slots handed out to rows (live edges + slack + rows' old places) */
+    uint64_t pool_capacity;        /* slots allocated */
+    uint64_t last_moved_row_slots; /* slots given to rows that outgrew their place in the last batch */
+    uint64_t repacks;              /* pool repacks (fresh slack for every row) so far */
 } wharf_stats;
 
 typedef struct wharf_handle wharf_handle;

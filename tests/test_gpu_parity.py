@@ -355,10 +355,10 @@ def test_affected_ids_on_device_match_host_list(W):
     gd.destroy()
 
 
-# (WHARF_N2V_REWALK, WHARF_MOVE_NO_LDS, WHARF_FORCE_RECORD_REBUILD, neighbour filter, WHARF_NO_MEMO,
+# (WHARF_N2V_REWALK, WHARF_NO_ROW_SLACK, WHARF_POOL_NO_HEADROOM, neighbour filter, WHARF_NO_MEMO,
 #  WHARF_NO_CHUNKED_SCAN)
-PATHS = {"sorted/patch-lds": ("sorted", "0", "0", "on", "1", "0"), "flat/inplace-l2": ("flat", "1", "1", "noslack", "0", "0"),
-         "sorted/inplace-lds": ("sorted", "0", "1", "off", "0", "1"), "flat/gather": ("flat", "1", "2", "on", "1", "1")}
+PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0"), "flat/move": ("flat", "1", "0", "noslack", "0", "0"),
+         "sorted/repack": ("sorted", "1", "1", "off", "0", "1"), "flat/slack-repack": ("flat", "0", "1", "on", "1", "1")}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -368,24 +368,25 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     corpus, counters, affected ids and CSR.  Re-walk: the interleaved sweep
     (DeepWalk, deterministic); for node2vec the planned, sorted re-walk list
     swept in lock step (k_rewalk_sorted) or by lanes at their own pace
-    (WHARF_N2V_REWALK=flat, k_rewalk_list).  CSR update: the record patch with the source table in
-    LDS or the bucketed L2 table (WHARF_MOVE_NO_LDS), into a second record
-    buffer, in place (chunked), or records rebuilt by a gather with node2vec
-    anchors kept aside (WHARF_FORCE_RECORD_REBUILD=1 / 2).  node2vec anchor
-    inits with the per-row neighbour filters (re-filled per source row, or with
-    no pool headroom re-built whole whenever a row outgrows its words) and
-    without them.  Deterministic re-walks by suffix table (k_rewalk_chunked
-    copy) and by walking every suffix (WHARF_NO_MEMO=1, k_rewalk_sweep).
-    Rewalk points alone (apply_walk_updates = false): the chunked scan, or
-    with WHARF_NO_CHUNKED_SCAN=1 the sweep kernels in scan-only mode."""
-    n2v_list, no_lds, force, filt, no_memo, no_chunked = PATHS[path]
+    (WHARF_N2V_REWALK=flat, k_rewalk_list).  CSR update (slack rows): rows
+    merged in place within their slack, rows without slack that move to the
+    pool's end on every insert (WHARF_NO_ROW_SLACK=1), and a pool without
+    headroom that is repacked whenever a row moves (WHARF_POOL_NO_HEADROOM=1,
+    node2vec anchors carried along).  node2vec anchor inits with the per-row
+    neighbour filters (re-filled per source row, or with no pool headroom
+    re-built whole whenever a row outgrows its words) and without them.
+    Deterministic re-walks by suffix table (k_rewalk_chunked copy) and by
+    walking every suffix (WHARF_NO_MEMO=1, k_rewalk_sweep).  Rewalk points
+    alone (apply_walk_updates = false): the chunked scan, or with
+    WHARF_NO_CHUNKED_SCAN=1 the sweep kernels in scan-only mode."""
+    n2v_list, no_slack, no_headroom, filt, no_memo, no_chunked = PATHS[path]
     monkeypatch.setenv("WHARF_NO_MEMO", no_memo)
     monkeypatch.setenv("WHARF_NO_CHUNKED_SCAN", no_chunked)
     monkeypatch.setenv("WHARF_NO_NEIGHBOUR_FILTER", "1" if filt == "off" else "0")
     monkeypatch.setenv("WHARF_FILTER_NO_SLACK", "1" if filt == "noslack" else "0")
     monkeypatch.setenv("WHARF_N2V_REWALK", n2v_list)
-    monkeypatch.setenv("WHARF_MOVE_NO_LDS", no_lds)
-    monkeypatch.setenv("WHARF_FORCE_RECORD_REBUILD", force)
+    monkeypatch.setenv("WHARF_NO_ROW_SLACK", no_slack)
+    monkeypatch.setenv("WHARF_POOL_NO_HEADROOM", no_headroom)
     base = O.generate_batch_of_edges(50000, 1 << 13, 6, False, False)
     off, adj = O.csr_from_edges(1 << 12, base)
     batches = [(True, O.generate_batch_of_edges(800, 1 << 12, 11, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
@@ -397,17 +398,18 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     _compare_stream(W, off, adj, batches, wpv=3, L=40, **kw)
 
 
-@pytest.mark.parametrize("force", ["0", "1", "2"])   # record patch / in place / gather rebuild
-@pytest.mark.parametrize("init", [1, 2])             # BURNIN, WEIGHT: inits that read prev's row
-def test_node2vec_anchor_reset_with_prev_row(W, monkeypatch, force, init):
+@pytest.mark.parametrize("rows", ["slack", "move", "repack"])   # rows merged in place / moved / pool repacked
+@pytest.mark.parametrize("init", [1, 2])                        # BURNIN, WEIGHT: inits that read prev's row
+def test_node2vec_anchor_reset_with_prev_row(W, monkeypatch, rows, init):
     """The anchor of state (cur=c, prev=s) is cached in slot s->c of s's row.
     Directed batches make s a source while its targets are not: s's rebuilt
     row starts with empty entries, so (c, s) is re-initialised against s's new
     row with the same Philox proposals (c's row epoch is unchanged) — the
     shard-invariant rule of DESIGN.md §4 (the reference keeps c's sampler,
     initialised against s's row at the first visit).  Exercised on all three
-    record paths, bit-exact against the oracle, which restates the same rule."""
-    monkeypatch.setenv("WHARF_FORCE_RECORD_REBUILD", force)
+    row-update paths, bit-exact against the oracle, which restates the same rule."""
+    monkeypatch.setenv("WHARF_NO_ROW_SLACK", "0" if rows == "slack" else "1")
+    monkeypatch.setenv("WHARF_POOL_NO_HEADROOM", "1" if rows == "repack" else "0")
     base = O.generate_batch_of_edges(30000, 1 << 12, 21, False, False)
     off, adj = O.csr_from_edges(1 << 11, base)
     R, A = O.REMOVE_DUPS, O.APPLY_WALK_UPDATES

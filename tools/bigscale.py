@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--mixed", action="store_true", help="insert batch b, then delete it")
     ap.add_argument("--no-oracle", action="store_true")
     ap.add_argument("--det", action="store_true", help="deterministic mode (DeepWalk)")
+    ap.add_argument("--shard", type=int, default=1,
+                    help="keep only rank 0's walk shard of an N-way split (the per-GPU work of an N-GPU run; "
+                         "the CSR stays whole, as on every rank)")
     a = ap.parse_args()
     import torch
     import dynamicgraphrepresentationlearning_amd as W
@@ -54,12 +57,18 @@ def main():
     m = g.number_of_edges()
     t_build = time.time() - t0
     print(f"graph n={n} m={m} built in {t_build:.1f}s", flush=True)
+    off, adj = g.flatten_graph()
+    deg = np.diff(off.astype(np.int64))
+    if a.shard > 1:
+        from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards
+        lo, hi = balanced_shards(deg, a.shard)[0]
+        g.set_shard(lo, hi)
+        print(f"shard 0 of {a.shard}: start vertices [{lo}, {hi}), {g.number_of_walks} walks", flush=True)
     g.generate_initial_random_walks()
     g.generate_initial_random_walks()
     st = g.stats()
-    off, adj = g.flatten_graph()
-    deg = np.diff(off.astype(np.int64))
-    active = int((deg > 0).sum()) * a.wpv
+    lo, hi = g.shard()[:2]
+    active = int((deg[lo:hi] > 0).sum()) * a.wpv
     ok_steps = st["steps"] == active * 79
     gen_rate = st["steps"] / st["last_walk_kernel_ms"] / 1e6
     print(f"generate: {st['last_walk_kernel_ms']:.1f} ms, steps {st['steps']} (expected {active * 79}), "
@@ -70,7 +79,7 @@ def main():
           flush=True)
     # sampled transitions are edges
     rng = np.random.default_rng(1)
-    wids = rng.choice(g.number_of_walks, 2000, replace=False)
+    wids = rng.choice(g.walk_ids(), 2000, replace=False)   # global ids of the owned walks
     bad = 0
     for w in wids:
         v = g.walk_vertices(int(w))
@@ -81,7 +90,7 @@ def main():
     print(f"sampled transitions not in the graph: {bad}", flush=True)
     # oracle re-computes a window of walks on the same (downloaded) CSR
     same = None
-    if not node2vec and not a.no_oracle:
+    if not node2vec and not a.no_oracle and a.shard == 1:
         w0 = int(n // 3)
         ref = O.Engine(off, adj, wpv=a.wpv, L=80, deterministic=a.det, seed=11)
         ref.time_generate_range(w0, w0 + 2048)
@@ -112,13 +121,16 @@ def main():
             print(f"after batch 0: update buffers {m1['update_buffers_bytes'] / 2**30:.1f} GiB, scratch "
                   f"{m1['scratch_bytes'] / 2**30:.1f} GiB, free {free / 2**30:.1f} GiB", flush=True)
     m2 = g.number_of_edges()
+    pst = g.stats()
+    print(f"slot pool: {pst['pool_slots']} of {pst['pool_capacity']} slots handed out (m {m2}), "
+          f"repacks {pst['repacks']}, in-edge scan {pst['last_csr_move_ms']:.2f} ms", flush=True)
     last = W.generate_batch_of_edges(5000, n, a.batches - 1, False, False)
     g.delete_edges_batch(last, remove_dups=True, out=out)
     m3 = g.number_of_edges()
     res = {"config": f"RMAT scale {a.scale}, {a.samples} undirected samples (seed 4), {a.model} {'deterministic' if a.det else 'MH'}, wpv {a.wpv}, "
                      f"L 80, {a.batches} {'insert+delete' if a.mixed else 'insert'} batches of "
                      "generate_batch_of_edges(5000, n, b, false, false)",
-           "n": n, "m": m, "walks": g.number_of_walks, "build_s": round(t_build, 1),
+           "n": n, "m": m, "walks": g.number_of_walks, "shard_of": a.shard, "build_s": round(t_build, 1),
            "gen_ms": round(st["last_walk_kernel_ms"], 2), "gen_Gsteps_per_s": round(gen_rate, 2),
            "steps_ok": ok_steps, "bad_transitions": bad, "oracle_window_identical": same,
            "batch_median_ms": round(float(np.median(lat)), 2), "batch_p90_ms": round(float(np.percentile(lat, 90)), 2),
@@ -126,7 +138,8 @@ def main():
            "walk_update_median_ms": round(float(np.median(wms)), 2),
            "mean_affected": int(np.mean(affs)),
            "rewalk_Gsteps_per_s": round(float(np.sum(steps) / np.sum(wms) / 1e6), 2),
-           "m_after_batches": m2, "m_after_delete_last": m3, "device_bytes_total": mem["total_bytes"]}
+           "m_after_batches": m2, "pool_slots": pst["pool_slots"], "pool_capacity": pst["pool_capacity"],
+           "repacks": pst["repacks"], "m_after_delete_last": m3, "device_bytes_total": mem["total_bytes"]}
     print(json.dumps(res), flush=True)
     assert ok_steps and bad == 0 and same in (True, None) and m3 <= m2
     g.destroy()

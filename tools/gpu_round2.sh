@@ -22,6 +22,9 @@ for s in "$@"; do
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 900 python bench.py ;;
     dist2)  step bench_dist2 900 env WHARF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --rewalk-batches 5 --det-rewalk-batches 3 ;;
+    c3shard8) step c3_shard8 900 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 5 --shard 8 ;;
+    c4shard8) step c4_n2v_shard8 900 python tools/bigscale.py --model node2vec --wpv 1 --batches 3 --mixed --no-oracle --shard 8 ;;
+    c3det8) step c3_det_shard8 900 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 5 --det --shard 8 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
