@@ -237,7 +237,7 @@ struct wharf_handle {
         build_records();
         if (anchors) build_edge_hash();
         if (anchors) build_filters();
-        bitmap.ensure((bitmap_words() + kBloomWords) * 4);   // exact bitmap, then the Bloom filter
+        bitmap.ensure((bitmap_words() + kFilterWords) * 4);   // exact bitmap, then the Bloom filter
         sync();
     }
 
@@ -651,7 +651,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         const int slack = wharf_handle::row_slack();
         uint64_t grow = 0, saved = 0;
         for (int attempt = 0;; attempt++) {
-            HIPCHK(hipMemsetAsync(h->bitmap.p, 0, (h->bitmap_words() + kBloomWords) * 4, s));
+            HIPCHK(hipMemsetAsync(h->bitmap.p, 0, (h->bitmap_words() + kFilterWords) * 4, s));
             launch_run_info(bkeys, h->runstart.as<uint32_t>(), k, mb, h->off.as<uint64_t>(), h->deg.as<uint32_t>(),
                             h->runs.as<RunInfo>(), h->bitmap.as<uint32_t>(), h->bitmap.as<uint32_t>() + h->bitmap_words(),
                             h->row_epoch.as<uint32_t>(), h->epoch, s);
@@ -884,7 +884,7 @@ int wharf_batch_walk_update(wharf_handle* h, const uint32_t* sources, uint64_t k
         REQUIRE(src.empty() || src.back() < h->n, WHARF_E_INVALID, "source vertex >= number_of_vertices()");
         k = src.size();
         hipStream_t s = h->s;
-        HIPCHK(hipMemsetAsync(h->bitmap.p, 0, (h->bitmap_words() + kBloomWords) * 4, s));
+        HIPCHK(hipMemsetAsync(h->bitmap.p, 0, (h->bitmap_words() + kFilterWords) * 4, s));
         if (k) {
             h->k1.ensure(k * 4);
             HIPCHK(hipMemcpyAsync(h->k1.p, src.data(), k * 4, hipMemcpyHostToDevice, s));

@@ -28,9 +28,32 @@ __host__ __device__ __forceinline__ uint32_t row_cap_initial(uint32_t d)
 }
 __host__ __device__ __forceinline__ uint32_t row_cap_grown(uint32_t d) { return d + ((d >> 3) > 4u ? (d >> 3) : 4u); }
 
-// two 17-bit hashes (k = 2: ~2 % false positives at 10 k sources in 2^17 bits)
-__host__ __device__ __forceinline__ uint32_t bloom_hash(uint32_t x) { return (x * 2654435761u) >> 15; }
-__host__ __device__ __forceinline__ uint32_t bloom_hash2(uint32_t x) { return ((x ^ 0x5bd1e995u) * 0x9E3779B1u + 0x7f4a7c15u) >> 15; }
+// Blocked Bloom filter of the batch sources (kBloomWords 32-bit words, held
+// in LDS by the scans): a key sets two bits of ONE word, so a test is one LDS
+// read (~2-3 % false positives at 10 k sources)
+__host__ __device__ __forceinline__ uint32_t bloom_word(uint32_t x) { return (x * 2654435761u) >> 20; }
+__host__ __device__ __forceinline__ uint32_t bloom_bits(uint32_t x)
+{
+    const uint32_t h = (x ^ 0x5bd1e995u) * 0x9E3779B1u + 0x7f4a7c15u;
+    return (1u << (h >> 27)) | (1u << ((h >> 22) & 31u));
+}
+__device__ __forceinline__ bool bloom_test(const uint32_t* f, uint32_t x)
+{
+    const uint32_t b = bloom_bits(x);
+    return (f[bloom_word(x)] & b) == b;
+}
+static_assert(kBloomWords == 4096, "bloom_word yields 12 bits");
+// The same scheme over 4x the words (64 KiB) for the in-edge scan, whose
+// positives each cost a random bitmap read: ~0.2 % false positives
+constexpr uint32_t kBigBloomWords = 16384;
+__host__ __device__ __forceinline__ uint32_t bloom_word_big(uint32_t x) { return (x * 2654435761u) >> 18; }
+__device__ __forceinline__ bool bloom_test_big(const uint32_t* f, uint32_t x)
+{
+    const uint32_t b = bloom_bits(x);
+    return (f[bloom_word_big(x)] & b) == b;
+}
+// bitmap buffer: [exact bitmap][kBloomWords][kBigBloomWords]
+constexpr uint32_t kFilterWords = kBloomWords + kBigBloomWords;
 
 // Philox counter word 3 = (epoch << 4) | stream
 enum : uint32_t { kStreamStep = 0, kStreamAnchor = 1, kStreamBurnin = 2, kStreamPrev = 3 };

@@ -494,8 +494,7 @@ __device__ __forceinline__ void bloom_to_lds(const WalkArgs& a, uint32_t* s_bloo
 
 __device__ __forceinline__ bool is_source(const WalkArgs& a, const uint32_t* s_bloom, uint32_t x)
 {
-    const uint32_t h = bloom_hash(x), h2 = bloom_hash2(x);
-    if (!((s_bloom[h >> 5] >> (h & 31)) & (s_bloom[h2 >> 5] >> (h2 & 31)) & 1u)) return false;
+    if (!bloom_test(s_bloom, x)) return false;
     return (a.bitmap[x >> 5] >> (x & 31)) & 1u;
 }
 
@@ -636,8 +635,7 @@ __device__ __forceinline__ uint32_t scan_chunk(const WalkArgs& a, const uint32_t
     uint32_t mask = 0, end = cnt;
 #pragma unroll
     for (uint32_t j = 0; j < kScanChunk; j++) {
-        const uint32_t h = bloom_hash(x[j]), h2 = bloom_hash2(x[j]);
-        mask |= ((s_bloom[h >> 5] >> (h & 31)) & (s_bloom[h2 >> 5] >> (h2 & 31)) & 1u) << j;
+        mask |= (uint32_t)bloom_test(s_bloom, x[j]) << j;
         if (x[j] == kSent && j < end) end = j;
     }
     if (end < 32) mask &= (1u << end) - 1u;
@@ -1321,9 +1319,8 @@ __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* _
         ri.src = s; ri.rs = rs; ri.re = re; ri.off = off[s]; ri.end = off[s] + deg[s];
         runs[j] = ri;
         atomicOr(bitmap + (s >> 5), 1u << (s & 31));
-        const uint32_t h = bloom_hash(s), h2 = bloom_hash2(s);
-        atomicOr(bloom + (h >> 5), 1u << (h & 31));
-        atomicOr(bloom + (h2 >> 5), 1u << (h2 & 31));
+        atomicOr(bloom + bloom_word(s), bloom_bits(s));
+        atomicOr(bloom + kBloomWords + bloom_word_big(s), bloom_bits(s));
         if (row_epoch) row_epoch[s] = epoch;   // the source's samplers are reset (wharfmh.h:504,539)
     }
 }
@@ -1339,9 +1336,8 @@ __global__ void k_mark_sources(const uint32_t* __restrict__ src, uint64_t k, Run
         ri.src = s;
         runs[j] = ri;
         atomicOr(bitmap + (s >> 5), 1u << (s & 31));
-        const uint32_t h = bloom_hash(s), h2 = bloom_hash2(s);
-        atomicOr(bloom + (h >> 5), 1u << (h & 31));
-        atomicOr(bloom + (h2 >> 5), 1u << (h2 & 31));
+        atomicOr(bloom + bloom_word(s), bloom_bits(s));
+        atomicOr(bloom + kBloomWords + bloom_word_big(s), bloom_bits(s));
     }
 }
 
@@ -1545,37 +1541,41 @@ __global__ void k_erec_rows(const RunInfo* __restrict__ runs, const uint64_t* __
 // checked against the new row epoch, anchor_lookup).  One streaming pass over
 // the pool's targets, four slots per 16-B load; the Bloom filter of the
 // sources sits in LDS and only its positives read the exact bitmap.
-__device__ __forceinline__ void patch_slot(uint32_t t, uint64_t e, const uint32_t* s_bloom, const uint32_t* bitmap,
-                                           const ERec* vrec, ERec* erec, uint32_t rs)
+__device__ __forceinline__ void patch_slot(uint32_t t, uint64_t e, const uint32_t* bitmap, const ERec* vrec, ERec* erec,
+                                           uint32_t rs)
 {
-    if (t == kGap) return;
-    const uint32_t h = bloom_hash(t), h2 = bloom_hash2(t);
-    if (!((s_bloom[h >> 5] >> (h & 31)) & (s_bloom[h2 >> 5] >> (h2 & 31)) & 1u)) return;
-    if (!((bitmap[t >> 5] >> (t & 31)) & 1u)) return;
-    erec[e * rs] = vrec[t];
+    if (t != kGap && ((bitmap[t >> 5] >> (t & 31)) & 1u)) erec[e * rs] = vrec[t];
 }
 
-__global__ __launch_bounds__(256) void k_patch_in_edges(const uint32_t* __restrict__ adj, uint64_t slots,
-                                                       const uint32_t* __restrict__ bitmap,
-                                                       const uint32_t* __restrict__ bloom,
-                                                       const ERec* __restrict__ vrec, ERec* __restrict__ erec,
-                                                       uint32_t rs)
+// 1024-thread workgroups, two per CU (the 64-KiB filter in LDS), 32 waves per CU
+__global__ __launch_bounds__(1024) void k_patch_in_edges(const uint32_t* __restrict__ adj, uint64_t slots,
+                                                        const uint32_t* __restrict__ bitmap,
+                                                        const uint32_t* __restrict__ bloom_big,
+                                                        const ERec* __restrict__ vrec, ERec* __restrict__ erec,
+                                                        uint32_t rs)
 {
-    __shared__ uint32_t s_bloom[kBloomWords];
-    for (uint32_t i = threadIdx.x; i < kBloomWords; i += blockDim.x) s_bloom[i] = bloom[i];
+    __shared__ uint32_t s_bloom[kBigBloomWords];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    for (uint32_t i = threadIdx.x; i < kBigBloomWords / 4; i += blockDim.x)
+        reinterpret_cast<u32x4*>(s_bloom)[i] = reinterpret_cast<const u32x4*>(bloom_big)[i];
     __syncthreads();
     const uint64_t n4 = slots / 4, stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const u32x4* __restrict__ a4 = reinterpret_cast<const u32x4*>(adj);
     for (uint64_t q = g; q < n4; q += stride) {
         const u32x4 t = __builtin_nontemporal_load(a4 + q);
-        patch_slot(t.x, 4 * q, s_bloom, bitmap, vrec, erec, rs);
-        patch_slot(t.y, 4 * q + 1, s_bloom, bitmap, vrec, erec, rs);
-        patch_slot(t.z, 4 * q + 2, s_bloom, bitmap, vrec, erec, rs);
-        patch_slot(t.w, 4 * q + 3, s_bloom, bitmap, vrec, erec, rs);
+        // Bloom-test the four slots branch-free (kGap may pass: the exact test rejects it)
+        const uint32_t hit = (uint32_t)bloom_test_big(s_bloom, t.x) | (uint32_t)bloom_test_big(s_bloom, t.y) << 1 |
+                             (uint32_t)bloom_test_big(s_bloom, t.z) << 2 | (uint32_t)bloom_test_big(s_bloom, t.w) << 3;
+        if (hit) {
+            for (uint32_t j = 0; j < 4; j++)
+                if ((hit >> j) & 1u) patch_slot(t[j], 4 * q + j, bitmap, vrec, erec, rs);
+        }
     }
-    if (g < slots - 4 * n4) patch_slot(adj[4 * n4 + g], 4 * n4 + g, s_bloom, bitmap, vrec, erec, rs);
+    if (g < slots - 4 * n4) {   // the pool's last < 4 slots
+        const uint32_t x = adj[4 * n4 + g];
+        if (bloom_test_big(s_bloom, x)) patch_slot(x, 4 * n4 + g, bitmap, vrec, erec, rs);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1867,8 +1867,8 @@ void launch_patch_in_edges(const uint32_t* adj, uint64_t slots, const uint32_t* 
                            const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s)
 {
     if (!slots) return;
-    const unsigned grid = (unsigned)std::min<uint64_t>((slots / 4 + 255) / 256 + 1, (uint64_t)cu_count() * 8);
-    hipLaunchKernelGGL(k_patch_in_edges, grid, 256, 0, s, adj, slots, bitmap, bloom, vrec, erec, rs);
+    const unsigned grid = (unsigned)std::min<uint64_t>((slots / 4 + 1023) / 1024 + 1, (uint64_t)cu_count() * 2);
+    hipLaunchKernelGGL(k_patch_in_edges, grid, 1024, 0, s, adj, slots, bitmap, bloom + kBloomWords, vrec, erec, rs);
 }
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s)
 {

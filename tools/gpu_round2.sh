@@ -25,6 +25,14 @@ for s in "$@"; do
     c3shard8) step c3_shard8 900 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 5 --shard 8 ;;
     c4shard8) step c4_n2v_shard8 900 python tools/bigscale.py --model node2vec --wpv 1 --batches 3 --mixed --no-oracle --shard 8 ;;
     c3det8) step c3_det_shard8 900 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 5 --det --shard 8 ;;
+    abscan) for v in cur ${AB:-}; do
+              lib=""; [ $v = cur ] || lib=tools/ab/lib_$v.so
+              step abscan_$v 600 env WHARF_LIB_PATH=$lib python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 1 --det --batches 4 --no-oracle
+            done ;;
+    probedet) for v in cur ${AB:-}; do
+              lib=""; [ $v = cur ] || lib=tools/ab/lib_$v.so
+              step probedet_$v 300 env WHARF_LIB_PATH=$lib python tools/rewalk_probe.py --det --batches 3
+            done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

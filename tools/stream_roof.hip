@@ -1,0 +1,163 @@
+// Streaming roof on MI355X for the update path's streaming kernels: what a
+// pass over a large u32 array reaches with the access shapes they use.
+//
+//   hipcc --offload-arch=gfx950 -O3 tools/stream_roof.hip -o tools/stream_roof && tools/stream_roof
+//
+//   sum      16-B loads per lane, grid-strided (U loads in flight per lane), XOR-reduced
+//   bloom    the same with the batch-source Bloom test of every element (LDS,
+//            k_patch_in_edges / scan_chunk): one LDS read + compare per element
+//   copy     16-B loads and stores (the det re-walk copy's byte budget)
+//   rows16   position-major [80][W] matrix, one lane per walk, 16 rows of a
+//            chunk loaded per round trip (k_rewalk_chunked<false>'s shape)
+// Each line: GB/s over the bytes moved, for workgroups-per-CU x U x non-temporal.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHK(x)                                                                   \
+    do {                                                                         \
+        hipError_t e = (x);                                                      \
+        if (e != hipSuccess) {                                                   \
+            std::printf("%s: %s\n", #x, hipGetErrorString(e));                   \
+            std::exit(1);                                                        \
+        }                                                                        \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kWords = 4096;
+
+__device__ __forceinline__ uint32_t bword(uint32_t x) { return (x * 2654435761u) >> 20; }
+__device__ __forceinline__ uint32_t bbits(uint32_t x)
+{
+    const uint32_t h = (x ^ 0x5bd1e995u) * 0x9E3779B1u + 0x7f4a7c15u;
+    return (1u << (h >> 27)) | (1u << ((h >> 22) & 31u));
+}
+
+__global__ void k_init(uint32_t* a, uint64_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        a[i] = (uint32_t)((i * 0x9E3779B97F4A7C15ull) >> 40);   // vertex-like ids < 2^24
+}
+
+template <int U, bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p)
+{
+    if (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+template <int U, bool NT, bool BLOOM>
+__global__ __launch_bounds__(256) void k_read(const uint32_t* __restrict__ a, uint64_t n, const uint32_t* __restrict__ f,
+                                              uint32_t* __restrict__ out)
+{
+    __shared__ uint32_t s[kWords];
+    if (BLOOM) {
+        for (uint32_t i = threadIdx.x; i < kWords; i += blockDim.x) s[i] = f[i];
+        __syncthreads();
+    }
+    const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
+    const u32x4* a4 = reinterpret_cast<const u32x4*>(a);
+    uint32_t acc = 0;
+    for (uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q0 < n4; q0 += stride * U) {
+        u32x4 t[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) t[u] = q0 + u * stride < n4 ? ld<U, NT>(a4 + q0 + u * stride) : u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (BLOOM) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t x = t[u][j], b = bbits(x);
+                    acc += (s[bword(x)] & b) == b;
+                }
+            } else {
+                acc ^= t[u].x ^ t[u].y ^ t[u].z ^ t[u].w;
+            }
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;   // keeps the loads alive
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void k_copy(const uint32_t* __restrict__ a, uint64_t n, uint32_t* __restrict__ b)
+{
+    const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
+    const u32x4* a4 = reinterpret_cast<const u32x4*>(a);
+    u32x4* b4 = reinterpret_cast<u32x4*>(b);
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
+        const u32x4 t = NT ? __builtin_nontemporal_load(a4 + q) : a4[q];
+        if (NT) __builtin_nontemporal_store(t, b4 + q);
+        else b4[q] = t;
+    }
+}
+
+// [L][W] position-major, lane = walk, C rows per round trip
+template <int C, bool NT>
+__global__ __launch_bounds__(256) void k_rows(const uint32_t* __restrict__ a, uint64_t W, uint32_t L,
+                                              uint32_t* __restrict__ out)
+{
+    uint32_t acc = 0;
+    for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += (uint64_t)gridDim.x * blockDim.x) {
+        for (uint32_t c0 = 0; c0 < L; c0 += C) {
+            uint32_t x[C];
+#pragma unroll
+            for (int j = 0; j < C; j++)
+                x[j] = c0 + j < L ? (NT ? __builtin_nontemporal_load(a + (uint64_t)(c0 + j) * W + li)
+                                        : a[(uint64_t)(c0 + j) * W + li])
+                                  : 0u;
+#pragma unroll
+            for (int j = 0; j < C; j++) acc ^= x[j];
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+int main(int argc, char** argv)
+{
+    const uint64_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 2560000000ull;   // configs[3] pool slots
+    const uint64_t W = 41943040;
+    const uint32_t L = 80;
+    uint32_t *a, *b, *f, *out;
+    CHK(hipMalloc(&a, n * 4));
+    CHK(hipMalloc(&b, W * L * 4 > n * 4 ? W * L * 4 : n * 4));
+    CHK(hipMalloc(&f, kWords * 4));
+    CHK(hipMalloc(&out, 64));
+    hipLaunchKernelGGL(k_init, 4096, 256, 0, 0, a, n);
+    hipLaunchKernelGGL(k_init, 4096, 256, 0, 0, b, W * L);
+    CHK(hipMemset(f, 0x11, kWords * 4));   // ~12 % of bits set (a 10 k-source filter has ~14 %)
+    CHK(hipDeviceSynchronize());
+    int cus = 0;
+    CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    hipEvent_t e0, e1;
+    CHK(hipEventCreate(&e0));
+    CHK(hipEventCreate(&e1));
+    auto time = [&](const char* what, int bpc, int u, int nt, double bytes, auto launch) {
+        float best = 1e30f;
+        for (int rep = 0; rep < 3; rep++) {
+            CHK(hipEventRecord(e0));
+            launch();
+            CHK(hipEventRecord(e1));
+            CHK(hipEventSynchronize(e1));
+            float ms;
+            CHK(hipEventElapsedTime(&ms, e0, e1));
+            if (ms < best) best = ms;
+        }
+        std::printf("{\"kernel\": \"%s\", \"wg_per_cu\": %d, \"U\": %d, \"nt\": %d, \"ms\": %.3f, \"GBps\": %.1f}\n", what,
+                    bpc, u, nt, best, bytes / best / 1e6);
+    };
+    for (int bpc : {4, 8, 16, 32}) {
+        const unsigned g = (unsigned)(cus * bpc);
+#define READ(U, NT, BL)                                                                                   \
+    time(BL ? "bloom" : "sum", bpc, U, NT, n * 4.0,                                                       \
+         [&] { hipLaunchKernelGGL((k_read<U, NT, BL>), g, 256, 0, 0, a, n, f, out); })
+        READ(1, true, false); READ(2, true, false); READ(4, true, false); READ(1, false, false); READ(4, false, false);
+        READ(1, true, true); READ(2, true, true); READ(4, true, true); READ(1, false, true);
+        time("copy", bpc, 1, 1, n * 8.0, [&] { hipLaunchKernelGGL(k_copy<true>, g, 256, 0, 0, a, n, b); });
+        time("copy", bpc, 1, 0, n * 8.0, [&] { hipLaunchKernelGGL(k_copy<false>, g, 256, 0, 0, a, n, b); });
+        time("rows16", bpc, 16, 1, W * L * 4.0, [&] { hipLaunchKernelGGL((k_rows<16, true>), g, 256, 0, 0, b, W, L, out); });
+        time("rows16", bpc, 16, 0, W * L * 4.0, [&] { hipLaunchKernelGGL((k_rows<16, false>), g, 256, 0, 0, b, W, L, out); });
+        time("rows8", bpc, 8, 1, W * L * 4.0, [&] { hipLaunchKernelGGL((k_rows<8, true>), g, 256, 0, 0, b, W, L, out); });
+    }
+    return 0;
+}
