@@ -33,6 +33,11 @@ for s in "$@"; do
               lib=""; [ $v = cur ] || lib=tools/ab/lib_$v.so
               step probedet_$v 300 env WHARF_LIB_PATH=$lib python tools/rewalk_probe.py --det --batches 3
             done ;;
+    pmcdet) DET="python3 tools/rewalk_probe.py --det --batches 2"
+            step pmcdet_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_rewalk_chunked" --output-format csv -d gpurun_out/pmcdet_fetch -o run -- $DET
+            step pmcdet_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_rewalk_chunked" --output-format csv -d gpurun_out/pmcdet_write -o run -- $DET
+            step pmcdet_sq 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "k_rewalk_chunked" --output-format csv -d gpurun_out/pmcdet_sq -o run -- $DET
+            step pmcdet_sq2 300 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_WAIT_ANY --kernel-include-regex "k_rewalk_chunked" --output-format csv -d gpurun_out/pmcdet_sq2 -o run -- $DET ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
