@@ -30,27 +30,27 @@ __host__ __device__ __forceinline__ uint32_t row_cap_grown(uint32_t d) { return 
 
 // Blocked Bloom filter of the batch sources (kBloomWords 32-bit words, held
 // in LDS by the scans): a key sets two bits of ONE word, so a test is one LDS
-// read (~2-3 % false positives at 10 k sources)
-__host__ __device__ __forceinline__ uint32_t bloom_word(uint32_t x) { return (x * 2654435761u) >> 20; }
-__host__ __device__ __forceinline__ uint32_t bloom_bits(uint32_t x)
-{
-    const uint32_t h = (x ^ 0x5bd1e995u) * 0x9E3779B1u + 0x7f4a7c15u;
-    return (1u << (h >> 27)) | (1u << ((h >> 22) & 31u));
-}
+// read (~2-3 % false positives at 10 k sources).  The scans are VALU-bound, so
+// the hash is one full-rate 24-bit multiply (v_mul_u32_u24; a 32-bit multiply
+// is quarter rate) of the id with its high bits folded in; the word comes from
+// the product's top bits, the two bit positions from bits 8-12 and 13-17.
+__device__ __forceinline__ uint32_t bloom_mix(uint32_t x) { return __umul24(x ^ (x >> 15), 0x9E3779u); }
+__device__ __forceinline__ uint32_t bloom_word(uint32_t h) { return h >> 20; }
+__device__ __forceinline__ uint32_t bloom_bits(uint32_t h) { return (1u << ((h >> 13) & 31u)) | (1u << ((h >> 8) & 31u)); }
 __device__ __forceinline__ bool bloom_test(const uint32_t* f, uint32_t x)
 {
-    const uint32_t b = bloom_bits(x);
-    return (f[bloom_word(x)] & b) == b;
+    const uint32_t h = bloom_mix(x), b = bloom_bits(h);
+    return (f[bloom_word(h)] & b) == b;
 }
 static_assert(kBloomWords == 4096, "bloom_word yields 12 bits");
 // The same scheme over 4x the words (64 KiB) for the in-edge scan, whose
 // positives each cost a random bitmap read: ~0.2 % false positives
 constexpr uint32_t kBigBloomWords = 16384;
-__host__ __device__ __forceinline__ uint32_t bloom_word_big(uint32_t x) { return (x * 2654435761u) >> 18; }
+__device__ __forceinline__ uint32_t bloom_word_big(uint32_t h) { return h >> 18; }
 __device__ __forceinline__ bool bloom_test_big(const uint32_t* f, uint32_t x)
 {
-    const uint32_t b = bloom_bits(x);
-    return (f[bloom_word_big(x)] & b) == b;
+    const uint32_t h = bloom_mix(x), b = bloom_bits(h);
+    return (f[bloom_word_big(h)] & b) == b;
 }
 // bitmap buffer: [exact bitmap][kBloomWords][kBigBloomWords]
 constexpr uint32_t kFilterWords = kBloomWords + kBigBloomWords;

@@ -604,6 +604,10 @@ __global__ __launch_bounds__(256) void k_det_suffix(WalkArgs a)
 #define WHARF_CHUNK_NT 3   // bit 0: non-temporal walk loads, bit 1: stores (A/B: -2..-3 % on the copy)
 #endif
 constexpr uint32_t kScanChunk = WHARF_SCAN_CHUNK;
+#ifndef WHARF_COPY_GROUP
+#define WHARF_COPY_GROUP 64   // lanes whose row segment the suffix copy writes together
+#endif
+constexpr uint32_t kCopyGroup = WHARF_COPY_GROUP;
 __device__ __forceinline__ uint32_t walk_load(const uint32_t* p)
 {
     if (WHARF_CHUNK_NT & 1) return __builtin_nontemporal_load(p);
@@ -613,6 +617,26 @@ __device__ __forceinline__ void walk_store(uint32_t* p, uint32_t v)
 {
     if (WHARF_CHUNK_NT & 2) __builtin_nontemporal_store(v, p);
     else *p = v;
+}
+// One walk-matrix row of a wave through a buffer resource: the row base (wave
+// uniform) sits in SGPRs and the lane adds its 32-bit byte offset, so the
+// address costs no VALU (a global access pays a 64-bit VALU add per row; the
+// chunked scans are VALU-bound).  aux 2 = non-temporal.
+#ifndef WHARF_ROW_BUFFER
+#define WHARF_ROW_BUFFER 0   // A/B (profiles/r02/chunked_scan): same scan time, copy 1-3 % slower
+#endif
+constexpr int kRowRsrcFlags = 0x00020000;   // gfx9 buffer descriptor word 3 (32-bit raw access)
+__device__ __forceinline__ uint32_t row_load(const uint32_t* row, uint32_t lane)
+{
+    if (!WHARF_ROW_BUFFER) return walk_load(row + lane);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)row, 0, 0x7FFFFFFF, kRowRsrcFlags);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, lane * 4, 0, (WHARF_CHUNK_NT & 1) ? 2 : 0);
+}
+__device__ __forceinline__ void row_store(uint32_t* row, uint32_t lane, uint32_t v)
+{
+    if (!WHARF_ROW_BUFFER) { walk_store(row + lane, v); return; }
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)row, 0, 0x7FFFFFFF, kRowRsrcFlags);
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane * 4, 0, (WHARF_CHUNK_NT & 2) ? 2 : 0);
 }
 static_assert(kMemoPad >= kScanChunk, "suffix table padding");
 static_assert(kScanChunk % 4 == 0 && kScanChunk <= 32, "chunk positions live in a 32-bit mask");
@@ -649,6 +673,13 @@ __device__ __forceinline__ uint32_t scan_chunk(const WalkArgs& a, const uint32_t
     return kScanChunk;
 }
 
+// a wave-uniform 64-bit value (from the first active lane) in SGPRs
+__device__ __forceinline__ uint64_t uniform64(uint64_t x)
+{
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x), hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // XCD-aware walk ranges: workgroup b runs on XCD b % 8, which takes the
 // (b % 8)-th eighth of the walks (whole 256-walk blocks, so rows stay aligned).
 struct XcdRange {
@@ -675,17 +706,22 @@ __global__ __launch_bounds__(256) void k_rewalk_chunked(WalkArgs a)
     const uint64_t W = a.W;
     const uint32_t L = a.L;
     const XcdRange xr = xcd_range(W);
+    const uint32_t lane = __lane_id();
     for (uint64_t li = xr.first; li < xr.end; li += xr.stride) {
         const uint64_t r = li / a.n_loc;
         uint32_t p = kNoRewalk;
         bool scanning = true;
         const uint32_t* __restrict__ row = nullptr;   // suffix row shifted by -p: the new value at pos is row[pos]
+        // the wave's columns start at a uniform base: row addresses live in
+        // SGPRs, the lane adds a 32-bit offset (no 64-bit VALU address math)
+        uint32_t* __restrict__ wb = walks + uniform64(li - lane);
         uint32_t cur[C], nxt[C];
 #pragma unroll
-        for (uint32_t j = 0; j < C; j++) cur[j] = j < L ? walk_load(walks + (uint64_t)j * W + li) : kSent;
+        for (uint32_t j = 0; j < C; j++) cur[j] = j < L ? row_load(wb + (uint64_t)j * W, lane) : kSent;
         for (uint32_t c0 = 0; c0 < L; c0 += C) {
             const uint32_t cnt = min(C, L - c0);
             const bool was_scanning = scanning;
+            const bool more = c0 + C < L;
             if (scanning) {
                 bool ended = false;
                 const uint32_t j = scan_chunk(a, s_bloom, cur, cnt, ended);
@@ -713,23 +749,27 @@ __global__ __launch_bounds__(256) void k_rewalk_chunked(WalkArgs a)
                 }
             }
             // next chunk's rows, in flight while this chunk is written
-            const bool more = c0 + C < L;
             if (more && scanning) {
 #pragma unroll
                 for (uint32_t j = 0; j < C; j++)
-                    nxt[j] = c0 + C + j < L ? walk_load(walks + (uint64_t)(c0 + C + j) * W + li) : kSent;
+                    nxt[j] = c0 + C + j < L ? row_load(wb + (uint64_t)(c0 + C + j) * W, lane) : kSent;
             }
             if (COPY) {
 #pragma unroll
                 for (uint32_t j = 0; j < C; j++) {
                     const uint32_t pos = c0 + j;
-                    if (j < cnt && __any(p < pos)) {
+                    // a row segment is written when one of its lanes re-walks this
+                    // position: whole 256-B rows (kCopyGroup 64) or 64-B quarters
+                    const uint64_t need = __ballot(p < pos);
+                    const uint32_t sh = (__lane_id() / kCopyGroup) * kCopyGroup;
+                    const uint64_t gm = (~0ull >> (64 - kCopyGroup)) << sh;
+                    if (j < cnt && (need & gm)) {
                         uint32_t val = was_scanning ? cur[j] : kSent;
                         if (p < pos) {
                             val = mv[j];
                             steps += val != kSent;
                         }
-                        walk_store(walks + (uint64_t)pos * W + li, val);
+                        row_store(wb + (uint64_t)pos * W, lane, val);
                     }
                 }
             }
@@ -1319,8 +1359,9 @@ __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* _
         ri.src = s; ri.rs = rs; ri.re = re; ri.off = off[s]; ri.end = off[s] + deg[s];
         runs[j] = ri;
         atomicOr(bitmap + (s >> 5), 1u << (s & 31));
-        atomicOr(bloom + bloom_word(s), bloom_bits(s));
-        atomicOr(bloom + kBloomWords + bloom_word_big(s), bloom_bits(s));
+        const uint32_t h = bloom_mix(s);
+        atomicOr(bloom + bloom_word(h), bloom_bits(h));
+        atomicOr(bloom + kBloomWords + bloom_word_big(h), bloom_bits(h));
         if (row_epoch) row_epoch[s] = epoch;   // the source's samplers are reset (wharfmh.h:504,539)
     }
 }
@@ -1336,8 +1377,9 @@ __global__ void k_mark_sources(const uint32_t* __restrict__ src, uint64_t k, Run
         ri.src = s;
         runs[j] = ri;
         atomicOr(bitmap + (s >> 5), 1u << (s & 31));
-        atomicOr(bloom + bloom_word(s), bloom_bits(s));
-        atomicOr(bloom + kBloomWords + bloom_word_big(s), bloom_bits(s));
+        const uint32_t h = bloom_mix(s);
+        atomicOr(bloom + bloom_word(h), bloom_bits(h));
+        atomicOr(bloom + kBloomWords + bloom_word_big(h), bloom_bits(h));
     }
 }
 
