@@ -234,18 +234,22 @@ int main(int argc, char** argv)
     CHK(hipEventCreate(&e0));
     CHK(hipEventCreate(&e1));
     auto time = [&](const char* what, int bpc, int u, int nt, double bytes, auto launch) {
-        float best = 1e30f;
+        float best = 1e30f, first = 0;
         for (int rep = 0; rep < 3; rep++) {
+            // between launches, touch 4 GB elsewhere (as the update pipeline does), so
+            // the first timed launch also meets cold TLBs and caches
+            if (rep == 0) hipLaunchKernelGGL(k_init, 4096, 256, 0, 0, a, (uint64_t)1 << 30);
             CHK(hipEventRecord(e0));
             launch();
             CHK(hipEventRecord(e1));
             CHK(hipEventSynchronize(e1));
             float ms;
             CHK(hipEventElapsedTime(&ms, e0, e1));
+            if (rep == 0) first = ms;
             if (ms < best) best = ms;
         }
-        std::printf("{\"kernel\": \"%s\", \"wg_per_cu\": %d, \"U\": %d, \"nt\": %d, \"ms\": %.3f, \"GBps\": %.1f}\n", what,
-                    bpc, u, nt, best, bytes / best / 1e6);
+        std::printf("{\"kernel\": \"%s\", \"wg_per_cu\": %d, \"U\": %d, \"nt\": %d, \"ms\": %.3f, \"GBps\": %.1f, "
+                    "\"first_ms\": %.3f}\n", what, bpc, u, nt, best, bytes / best / 1e6, first);
     };
     {
         uint32_t *bm, *bl;
