@@ -180,6 +180,43 @@ def cpu_baseline(args, n, active_vertices, off, adj, kind):
                       f"{steps} steps in {secs:.2f} s", "seconds": secs}
 
 
+def cpu_baseline_deterministic(args, batches=3):
+    """The reference's default mode (config::deterministic_mode = true,
+    globals.h:29) on the reference CPU path: configs[2]'s graph, generation and
+    10k-edge insert batches with the walk update applied, on a bounded sample
+    (1 walk per vertex of length --cpu-length; the GPU line runs 10 x 80), so
+    it finishes in well under a minute.  Reported beside the GPU's
+    deterministic re-walk latency, not compared with it as the same workload."""
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    cores = cpu_cores(args.cpu_threads)
+    ns = 1 << args.scale
+    cmd = [harness, "cfg", "1", str(args.cpu_length), "deepwalk", str(args.paramP), str(args.paramQ), "weight", "1",
+           "42", "graph-rmat", str(args.stream_samples), str(2 * ns), str(args.seed + 1), str(ns), "time-gen", "1",
+           "time-upd", "5000", "0", "0", str(batches)]
+    log(f"cpu_baseline_deterministic: reference harness, {cores} threads: {' '.join(cmd[1:])}")
+    try:
+        r = subprocess.run(cmd, env=dict(os.environ, NUM_THREADS=str(cores)), capture_output=True, text=True,
+                           timeout=args.cpu_timeout)
+    except subprocess.TimeoutExpired:
+        log("cpu_baseline_deterministic: harness timed out")
+        return None
+    gen = re.search(r"time-gen seconds=([0-9.]+)", r.stdout)
+    upd = [(float(a), int(b)) for a, b in re.findall(r"time-upd seconds=([0-9.]+) edges=\d+ affected=(\d+)", r.stdout)]
+    if r.returncode != 0 or not gen or not upd:
+        log("cpu_baseline_deterministic: harness failed", r.returncode, r.stderr[-500:])
+        return None
+    return {"kind": "reference", "cores": cores,
+            "sample": f"reference WharfMH, deterministic mode, configs[2]'s graph (RMAT scale {args.scale}, "
+                      f"{args.stream_samples} undirected samples), walks_per_vertex=1, L={args.cpu_length} "
+                      f"(the GPU line: {args.wpv} x {args.length}); {batches} insert batches of "
+                      f"generate_batch_of_edges(5000, n, b, false, undirected), walk update applied",
+            "generation_seconds": float(gen.group(1)),
+            "insert_batch_median_ms": round(float(np.median([u[0] for u in upd])) * 1e3, 1),
+            "mean_affected_walks": int(np.mean([u[1] for u in upd]))}
+
+
 def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrier, batches, scan_batches=0):
     """configs[2]: per-batch latency of 10k-edge insert batches with the re-walk applied
     (memory-throughput-latency.cpp:126-134: generate_batch_of_edges(5000, n, seed=b, false, undirected))."""
@@ -501,6 +538,8 @@ def main():
         if world == 1 and args.cpu_baseline != "off":
             active = int((deg > 0).sum())
             line["cpu_baseline"] = cpu_baseline(args, n, active, off, adj, args.cpu_baseline)
+            if args.cpu_baseline in ("auto", "reference") and args.det_rewalk_batches > 0:
+                line["cpu_baseline_deterministic"] = cpu_baseline_deterministic(args)
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

@@ -29,6 +29,9 @@
 //   dump-graph                                 flattened CSR
 //   walkstr <wid>                              WharfMH::walk(wid) text to walkstr_<k>.txt
 //   time-gen <reps>                            time generate_initial_random_walks
+//   time-upd <M> <seed> <directed 0|1> <reps>  time insert_edges_batch of RMAT batches
+//                                              (seeds seed, seed+1, ...; walk update applied,
+//                                              nothing dumped)
 //   kat                                        RNG / hash / Szudzik / RMAT known answers
 //   batch <M> <V> <seed> <directed>            dump generate_batch_of_edges output
 #include <wharfmh.h>
@@ -282,6 +285,21 @@ int main(int argc, char** argv)
                 std::printf("time-gen seconds=%.6f walks=%zu L=%d workers=%d\n", s,
                             g_n * (size_t)config::walks_per_vertex, (int)config::walk_length, (int)num_workers());
                 std::fflush(stdout);
+            }
+        } else if (c == "time-upd") {
+            size_t M = std::stoull(a[i++]), seed = std::stoull(a[i++]);
+            bool directed = std::stoi(a[i++]) != 0;
+            int reps = std::stoi(a[i++]);
+            size_t pow2 = 1ul << (pbbs::log2_up(g_n) - 1);
+            for (int r = 0; r < reps; r++) {
+                auto b = utility::generate_batch_of_edges(M, g_n, seed + r, false, directed);
+                auto t0 = std::chrono::steady_clock::now();
+                auto aff = g_w->insert_edges_batch(b.second, b.first, false, true, pow2);
+                double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                std::printf("time-upd seconds=%.6f edges=%zu affected=%zu workers=%d\n", s, b.second, aff.size(),
+                            (int)num_workers());
+                std::fflush(stdout);
+                pbbs::free_array(b.first);
             }
         } else if (c == "kat") {
             do_kat();
