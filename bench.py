@@ -119,15 +119,21 @@ def gather_ceiling(steps_per_s: float, live: float | None):
             "source": "profiles/gather_ceiling.json (another box)"}
 
 
+PMC_ROUNDS = ("r02_", "")   # newest round's rocprofv3 summary first
+
+
 def load_traffic(tag: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(REPO, "profiles", f"pmc_{tag}.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        return json.load(open(path)).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (newest
+    round first), and the file it came from."""
+    for pre in PMC_ROUNDS:
+        rel = os.path.join("profiles", f"pmc_{pre}{tag}.json")
+        path = os.path.join(REPO, rel)
+        if os.path.exists(path):
+            try:
+                return json.load(open(path)).get("hbm_bytes_per_launch"), f"{rel} (rocprofv3 PMC pass)"
+            except Exception:
+                pass
+    return None, None
 
 
 def cpu_cores(requested: int) -> int:
@@ -336,6 +342,7 @@ def node2vec_record(args, W, torch, dev, barrier, n):
     steps = st["steps"]
     avg = float(np.mean(kern))
     achieved = steps * BYTES_PER_STEP_NODE2VEC / (avg * 1e-3) / 1e9
+    n2v_traffic, n2v_traffic_src = load_traffic(f"gen_node2vec_mh_s{args.scale}")
     rec = {"workload": f"configs[1] graph (RMAT scale {args.scale}, m={g.number_of_edges()}), node2vec "
                        f"p={args.paramP} q={args.paramQ} MH, WEIGHT sampler init, walks_per_vertex={args.wpv}, "
                        f"walk_length={args.length}",
@@ -346,15 +353,14 @@ def node2vec_record(args, W, torch, dev, barrier, n):
            "roofline": {"bound": "hbm", "kernel": "k_walk<node2vec, MH> (warm generation)",
                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "bytes_per_step": BYTES_PER_STEP_NODE2VEC,
-                        "traffic": load_traffic(f"gen_node2vec_mh_s{args.scale}"),
-                        "traffic_source": f"profiles/pmc_gen_node2vec_mh_s{args.scale}.json (rocprofv3 PMC pass)"}}
+                        "traffic": n2v_traffic, "traffic_source": n2v_traffic_src}}
     g.destroy()
     rec["rewalk_latency_10k_batch"] = stream_latency(args, W, torch, cfg, dev, 1, 0, None, None, barrier,
                                                      args.n2v_rewalk_batches)
     return rec
 
 
-def streaming_rooflines(rewalk, rewalk_det):
+def streaming_rooflines(rewalk, rewalk_det, scale):
     """The streaming kernels of the update path against the HBM peak, by
     algorithmic bytes (SURVEY 8(d)): rewalk-point scan 4 B per stored position;
     deterministic re-walk (suffix table + chunked copy) 4 B per stored position
@@ -362,22 +368,32 @@ def streaming_rooflines(rewalk, rewalk_det):
     in-edge record scan of the slack-row CSR update 4 B per pool slot (the
     slots' targets are read; the few records of sources' in-edges written)."""
     out = {}
-    def ent(kernel, bytes_, ms, per):
+    pmc_rel = os.path.join("profiles", f"pmc_r02_streaming_s{scale}.json")
+    pmc = json.load(open(os.path.join(REPO, pmc_rel))) if os.path.exists(os.path.join(REPO, pmc_rel)) else {}
+
+    def ent(name, kernel, bytes_, ms, per):
         if not ms:
             return None
         a = bytes_ / (ms * 1e-3) / 1e9
-        return {"kernel": kernel, "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(a / HBM_PEAK_GBS, 4), "ms": ms, "algorithmic_bytes": int(bytes_), "per_unit": per}
+        e = {"kernel": kernel, "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(a / HBM_PEAK_GBS, 4), "ms": ms, "algorithmic_bytes": int(bytes_), "per_unit": per,
+             "traffic": None}
+        if name in pmc:   # HBM bytes per launch (PMC pass of the same stream) and the rate they move at
+            e["traffic"] = pmc[name]["hbm_bytes_per_launch"]
+            e["traffic_GBps"] = round(e["traffic"] / (ms * 1e-3) / 1e9, 1)
+            e["traffic_source"] = f"{pmc_rel} (rocprofv3 PMC pass)"
+        return e
     if rewalk_det:
         pos = rewalk_det["stored_positions_rank0"]
-        out["rewalk_point_scan"] = ent("k_rewalk_chunked<false> (apply_walk_updates=false)", 4 * pos,
-                                       rewalk_det.get("scan_only_median_ms"), "4 B per stored position")
-        out["deterministic_rewalk_copy"] = ent("k_det_suffix + k_rewalk_chunked<true>", 4 * pos,
-                                               rewalk_det["median_rewalk_kernel_ms"], "4 B per stored position")
+        out["rewalk_point_scan"] = ent("rewalk_point_scan", "k_rewalk_chunked<false> (apply_walk_updates=false)",
+                                       4 * pos, rewalk_det.get("scan_only_median_ms"), "4 B per stored position")
+        out["deterministic_rewalk_copy"] = ent("deterministic_rewalk_copy", "k_det_suffix + k_rewalk_chunked<true>",
+                                               4 * pos, rewalk_det["median_rewalk_kernel_ms"],
+                                               "4 B per stored position")
     src = rewalk or rewalk_det
     if src:
-        out["in_edge_scan"] = ent("k_patch_in_edges (records of the batch sources' in-edges)", 4 * src["pool_slots"],
-                                  src["median_in_edge_scan_ms"], "4 B per pool slot")
+        out["in_edge_scan"] = ent("in_edge_scan", "k_patch_in_edges (records of the batch sources' in-edges)",
+                                  4 * src["pool_slots"], src["median_in_edge_scan_ms"], "4 B per pool slot")
     return out or None
 
 
@@ -494,7 +510,7 @@ def main():
             # re-walk steps (one gather each) against the same ceiling; the scan rides along
             rewalk["rewalk_frac_of_gather_ceiling"] = round(rewalk["rewalk_Gsteps_per_s"] / live_ceiling, 4)
         achieved = (steps_local * bytes_per_step / (avg_kernel_ms * 1e-3) / 1e9) if bytes_per_step else None
-        traffic = load_traffic(tag)
+        traffic, traffic_src = load_traffic(tag)
         line = {
             "metric": "MH walk-steps/sec" if not args.det else "deterministic walk-steps/sec",
             "value": round(value, 1),
@@ -519,7 +535,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_walk (generation)",
                          "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
-                         "traffic": traffic, "traffic_source": f"profiles/pmc_{tag}.json (rocprofv3 PMC pass)",
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "bytes_per_step": bytes_per_step,
                          "avg_kernel_ms": round(avg_kernel_ms, 3),
                          # the first generation of a fresh handle (node2vec: every anchor initialised)
@@ -531,7 +547,7 @@ def main():
             "mh_node2vec": n2v,
             "rewalk_latency_10k_batch": rewalk,
             "rewalk_latency_10k_batch_deterministic": rewalk_det,
-            "streaming_rooflines": streaming_rooflines(rewalk, rewalk_det),
+            "streaming_rooflines": streaming_rooflines(rewalk, rewalk_det, args.scale),
             "corpus_allgatherv": corpus,
             "cpu_baseline": None,
         }

@@ -38,6 +38,13 @@ for s in "$@"; do
             step pmcdet_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_rewalk_chunked" --output-format csv -d gpurun_out/pmcdet_write -o run -- $DET
             step pmcdet_sq 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex "k_rewalk_chunked" --output-format csv -d gpurun_out/pmcdet_sq -o run -- $DET
             step pmcdet_sq2 300 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_WAIT_ANY --kernel-include-regex "k_rewalk_chunked" --output-format csv -d gpurun_out/pmcdet_sq2 -o run -- $DET ;;
+    prof)   step prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py --cpu-baseline off ;;
+    pmc)    GEN="python3 bench.py --steps 2 --warmup 0 --rewalk-batches 0 --det-rewalk-batches 0 --n2v-steps 2 --n2v-rewalk-batches 0 --cpu-baseline off"
+            STR="python3 bench.py --steps 1 --warmup 0 --rewalk-batches 0 --det-rewalk-batches 3 --n2v-steps 0 --n2v-rewalk-batches 0 --cpu-baseline off"
+            step pmc_gen_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_walk" --output-format csv -d gpurun_out/pmc_gen_fetch -o run -- $GEN
+            step pmc_gen_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_walk" --output-format csv -d gpurun_out/pmc_gen_write -o run -- $GEN
+            step pmc_str_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_rewalk_chunked|k_patch_in_edges" --output-format csv -d gpurun_out/pmc_str_fetch -o run -- $STR
+            step pmc_str_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_rewalk_chunked|k_patch_in_edges" --output-format csv -d gpurun_out/pmc_str_write -o run -- $STR ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
