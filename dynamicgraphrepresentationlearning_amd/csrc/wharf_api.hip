@@ -100,7 +100,7 @@ struct wharf_handle {
     std::string err;
 
     void sync() { HIPCHK(hipStreamSynchronize(s)); }
-    uint64_t bitmap_words() const { return (n + 31) / 32 + 1; }
+    uint64_t bitmap_words() const { return (((n + 31) / 32 + 1) + 3) & ~3ull; }   // the filters after it stay 16-B aligned
 
     template <class F> void rp(F&& f)   // run a rocPRIM call with the shared temp buffer
     {

@@ -651,25 +651,56 @@ __device__ __forceinline__ uint32_t chunk_pick(const uint32_t (&x)[kScanChunk], 
     return v;
 }
 
-// First batch source among x[0..cnt) before the old walk's end, or kScanChunk
-// (then `ended` tells whether the walk ended inside the chunk).
-__device__ __forceinline__ uint32_t scan_chunk(const WalkArgs& a, const uint32_t* s_bloom,
-                                               const uint32_t (&x)[kScanChunk], uint32_t cnt, bool& ended)
+// Batch-source test of one chunk, in two halves so a caller can put the next
+// chunk's row loads between them.  chunk_issue: the Bloom test of every
+// position (LDS), then the exact bitmap word of every positive, all loads
+// independent (one round trip per chunk; the first version settled the
+// positives one dependent load at a time: ~3-4 round trips per chunk for a
+// wave, a third of the configs[2] scan's time).  chunk_resolve: the first
+// position whose bit is set, or kScanChunk (then `ended` tells whether the
+// old walk ended inside the chunk).
+#ifndef WHARF_SCAN_BATCH
+#define WHARF_SCAN_BATCH 1   // A/B: 0 = one dependent bitmap read per positive
+#endif
+struct ChunkTest {
+    uint32_t mask, end;
+    uint32_t w[kScanChunk];
+};
+
+__device__ __forceinline__ void chunk_issue(const WalkArgs& a, const uint32_t* s_bloom, const uint32_t (&x)[kScanChunk],
+                                            uint32_t cnt, ChunkTest& t)
 {
-    uint32_t mask = 0, end = cnt;
+    t.mask = 0;
+    t.end = cnt;
 #pragma unroll
     for (uint32_t j = 0; j < kScanChunk; j++) {
-        mask |= (uint32_t)bloom_test(s_bloom, x[j]) << j;
-        if (x[j] == kSent && j < end) end = j;
+        t.mask |= (uint32_t)bloom_test(s_bloom, x[j]) << j;
+        if (x[j] == kSent && j < t.end) t.end = j;
     }
-    if (end < 32) mask &= (1u << end) - 1u;
-    while (mask) {
+    if (t.end < 32) t.mask &= (1u << t.end) - 1u;
+#if WHARF_SCAN_BATCH
+#pragma unroll
+    for (uint32_t j = 0; j < kScanChunk; j++) t.w[j] = ((t.mask >> j) & 1u) ? a.bitmap[x[j] >> 5] : 0u;
+#endif
+}
+
+__device__ __forceinline__ uint32_t chunk_resolve(const WalkArgs& a, const uint32_t (&x)[kScanChunk], uint32_t cnt,
+                                                  const ChunkTest& t, bool& ended)
+{
+#if WHARF_SCAN_BATCH
+    uint32_t hit = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kScanChunk; j++) hit |= ((t.w[j] >> (x[j] & 31u)) & 1u) << j;
+    hit &= t.mask;
+    if (hit) return (uint32_t)__builtin_ctz(hit);
+#else
+    for (uint32_t mask = t.mask; mask; mask &= mask - 1u) {
         const uint32_t j = (uint32_t)__builtin_ctz(mask);
         const uint32_t v = chunk_pick(x, j);
         if ((a.bitmap[v >> 5] >> (v & 31)) & 1u) return j;
-        mask &= mask - 1u;
     }
-    ended = end < cnt;
+#endif
+    ended = t.end < cnt;
     return kScanChunk;
 }
 
@@ -695,8 +726,17 @@ __device__ __forceinline__ XcdRange xcd_range(uint64_t W)
 
 // COPY = false: rewalk points only (apply_walk_updates = false, any model).
 // COPY = true: deterministic re-walk from the suffix table (k_det_suffix).
+#ifndef WHARF_SCAN_WAVES_EU
+#define WHARF_SCAN_WAVES_EU 0   // A/B: force this many waves per SIMD on the scans (0 = compiler's choice)
+#endif
+#if WHARF_SCAN_WAVES_EU
+#define WHARF_SCAN_WAVES __attribute__((amdgpu_waves_per_eu(WHARF_SCAN_WAVES_EU, WHARF_SCAN_WAVES_EU)))
+#else
+#define WHARF_SCAN_WAVES
+#endif
+
 template <bool COPY>
-__global__ __launch_bounds__(256) void k_rewalk_chunked(WalkArgs a)
+__global__ __launch_bounds__(256) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArgs a)
 {
     constexpr uint32_t C = kScanChunk;
     __shared__ uint32_t s_bloom[kBloomWords];
@@ -722,9 +762,18 @@ __global__ __launch_bounds__(256) void k_rewalk_chunked(WalkArgs a)
             const uint32_t cnt = min(C, L - c0);
             const bool was_scanning = scanning;
             const bool more = c0 + C < L;
+            ChunkTest ct;
+            if (scanning) chunk_issue(a, s_bloom, cur, cnt, ct);
+            if (!COPY && more && scanning) {
+                // scan only: the next chunk's rows go out before the bitmap words
+                // are waited for (loads complete in order: the wait leaves them in flight)
+#pragma unroll
+                for (uint32_t j = 0; j < C; j++)
+                    nxt[j] = c0 + C + j < L ? row_load(wb + (uint64_t)(c0 + C + j) * W, lane) : kSent;
+            }
             if (scanning) {
                 bool ended = false;
-                const uint32_t j = scan_chunk(a, s_bloom, cur, cnt, ended);
+                const uint32_t j = chunk_resolve(a, cur, cnt, ct, ended);
                 if (j < C) {
                     p = c0 + j;
                     scanning = false;
@@ -749,7 +798,7 @@ __global__ __launch_bounds__(256) void k_rewalk_chunked(WalkArgs a)
                 }
             }
             // next chunk's rows, in flight while this chunk is written
-            if (more && scanning) {
+            if (COPY && more && scanning) {
 #pragma unroll
                 for (uint32_t j = 0; j < C; j++)
                     nxt[j] = c0 + C + j < L ? row_load(wb + (uint64_t)(c0 + C + j) * W, lane) : kSent;
@@ -774,7 +823,7 @@ __global__ __launch_bounds__(256) void k_rewalk_chunked(WalkArgs a)
                 }
             }
             if (!__any(scanning || (COPY && p != kNoRewalk))) break;
-            if (more && scanning) {
+            if (more && (COPY ? scanning : was_scanning)) {
 #pragma unroll
                 for (uint32_t j = 0; j < C; j++) cur[j] = nxt[j];
             }
@@ -819,7 +868,51 @@ void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStr
 // kernel over the same sorted list: 104 ms / 47.9 ms (scattered stores).
 constexpr uint64_t kListMask = (1ull << 40) - 1;   // counters[2]: tickets << 40 | list entries
 
-__global__ __launch_bounds__(256) void k_rewalk_plan(WalkArgs a)
+// The rewalk point of lane li's walk by the chunked scan of k_rewalk_chunked<false>
+// (kScanChunk rows per round trip, the next chunk's rows in flight while this
+// one's bitmap words are read).  Every lane of the wave calls it; lanes
+// without a walk (li >= W) with active = false.
+__device__ __forceinline__ uint32_t chunked_point(const WalkArgs& a, const uint32_t* s_bloom, uint64_t li, bool active)
+{
+    constexpr uint32_t C = kScanChunk;
+    const uint32_t L = a.L, lane = __lane_id();
+    const uint64_t W = a.W;
+    const uint32_t* __restrict__ wb = a.walks + uniform64(li - lane);
+    uint32_t p = kNoRewalk;
+    bool scanning = active;
+    uint32_t cur[C], nxt[C];
+#pragma unroll
+    for (uint32_t j = 0; j < C; j++) cur[j] = (scanning && j < L) ? row_load(wb + (uint64_t)j * W, lane) : kSent;
+    for (uint32_t c0 = 0; c0 < L; c0 += C) {
+        const uint32_t cnt = min(C, L - c0);
+        const bool more = c0 + C < L, was_scanning = scanning;
+        ChunkTest ct;
+        if (scanning) chunk_issue(a, s_bloom, cur, cnt, ct);
+        if (more && scanning) {
+#pragma unroll
+            for (uint32_t j = 0; j < C; j++)
+                nxt[j] = c0 + C + j < L ? row_load(wb + (uint64_t)(c0 + C + j) * W, lane) : kSent;
+        }
+        if (scanning) {
+            bool ended = false;
+            const uint32_t j = chunk_resolve(a, cur, cnt, ct, ended);
+            if (j < C) {
+                p = c0 + j;
+                scanning = false;
+            } else if (ended) {
+                scanning = false;
+            }
+        }
+        if (!__any(scanning)) break;
+        if (more && was_scanning) {
+#pragma unroll
+            for (uint32_t j = 0; j < C; j++) cur[j] = nxt[j];
+        }
+    }
+    return p;
+}
+
+__global__ __launch_bounds__(256) WHARF_SCAN_WAVES void k_rewalk_plan(WalkArgs a)
 {
     __shared__ uint32_t s_bloom[kBloomWords];
     __shared__ uint32_t s_bin[256];                        // count, then cursor, per rewalk point (255: none)
@@ -827,26 +920,14 @@ __global__ __launch_bounds__(256) void k_rewalk_plan(WalkArgs a)
     __shared__ unsigned long long s_ticket;
     bloom_to_lds(a, s_bloom);
     if (blockDim.x != 256) __builtin_trap();               // one histogram bin per thread
-    uint32_t* __restrict__ walks = a.walks;
     const uint64_t W = a.W;
     const uint32_t L = a.L, t = threadIdx.x, lane = __lane_id();
     for (uint64_t base = (uint64_t)blockIdx.x * 256; base < W; base += (uint64_t)gridDim.x * 256) {
         const uint64_t li = base + t;
-        uint32_t p = kNoRewalk;
-        if (li < W) {
-            const uint64_t r = li / a.n_loc;
-            uint32_t x = (uint32_t)(a.lo + (li - r * a.n_loc));
-            uint32_t xn = L > 1 ? walks[W + li] : kSent;   // next position, prefetched
-            for (uint32_t pos = 0; pos < L; pos++) {
-                if (pos > 0) {
-                    x = xn;
-                    if (x == kSent) break;
-                    if (pos + 1 < L) xn = walks[(uint64_t)(pos + 1) * W + li];
-                }
-                if (is_source(a, s_bloom, x)) { p = pos; break; }
-            }
-            a.aff[li] = (uint8_t)p;
-        }
+        // chunked scan (round 2: the one-row-prefetch scan it replaces was
+        // latency-bound, 7.5 ms per configs[2] node2vec batch)
+        const uint32_t p = chunked_point(a, s_bloom, li, li < W);
+        if (li < W) a.aff[li] = (uint8_t)p;
         if (a.scan_only) continue;
         const uint32_t key = (li < W && p + 1 < L) ? p : 255u;   // re-walking: something after the point
         s_bin[t] = 0;

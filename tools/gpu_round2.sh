@@ -45,6 +45,10 @@ for s in "$@"; do
             step pmc_gen_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_walk" --output-format csv -d gpurun_out/pmc_gen_write -o run -- $GEN
             step pmc_str_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_rewalk_chunked|k_patch_in_edges" --output-format csv -d gpurun_out/pmc_str_fetch -o run -- $STR
             step pmc_str_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_rewalk_chunked|k_patch_in_edges" --output-format csv -d gpurun_out/pmc_str_write -o run -- $STR ;;
+    proben2v) for v in cur ${AB:-}; do
+              lib=""; [ $v = cur ] || lib=tools/ab/lib_$v.so
+              step proben2v_$v 300 env WHARF_LIB_PATH=$lib python tools/rewalk_probe.py --model node2vec --batches 3
+            done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
