@@ -96,6 +96,8 @@ struct wharf_handle {
     uint64_t fpool_used = 0;                   // words handed out (rows that outgrew theirs leave gaps)
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
     DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, count, pairs, sel, defer, rplan, pscan, scratch;
+    DevBuf stab;                               // node2vec MH re-walk: start-state anchor table (k_rewalk_sorted)
+    uint64_t start_bound = 0;                  // distinct re-walk start states of the next walk update, at most (0: unknown)
     wharf_stats st{};
     std::string err;
 
@@ -464,7 +466,7 @@ void free_handle(wharf_handle* h)
                       &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->walks, &h->aff, &h->rtab,
                       &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags, &h->chg, &h->cf,
                       &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel, &h->defer, &h->rplan, &h->pscan,
-                      &h->scratch})
+                      &h->scratch, &h->stab})
         b->release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -532,7 +534,24 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         if (a.model == kNode2Vec && !a.det) {   // k_rewalk_plan's compacted, sorted re-walk list
             h->defer.ensure(h->W * 8);
             a.defer = h->defer.as<uint64_t>();
+            const char* no_stab = getenv("WHARF_NO_START_TABLE");   // A/B and tests: binary search at every start
+            if (!a.scan_only && k && !(no_stab && atoi(no_stab))) {
+                // start states (x, prev): x a batch source, prev an in-neighbour of it, so at most
+                // the sources' degrees (undirected) and the re-walking walks; twice that many
+                // entries, four per 64-B bucket (a full neighbourhood falls back to the search)
+                const uint64_t bound = std::min<uint64_t>(h->start_bound ? h->start_bound : h->W, h->W);
+                uint64_t buckets = 64;
+                while (buckets * 4 < 2 * bound && buckets < (1ull << 22)) buckets <<= 1;
+                const char* tb = getenv("WHARF_START_TABLE_BUCKETS");   // tests: a tiny table (overflow fallback)
+                if (tb && atoi(tb) > 0)
+                    for (buckets = 1; buckets < (uint64_t)atoi(tb);) buckets <<= 1;
+                h->stab.ensure(buckets * 64);
+                HIPCHK(hipMemsetAsync(h->stab.p, 0xFF, buckets * 64, s));   // keys kStabEmpty, entries kAnchorNone64
+                a.stab = h->stab.as<uint64_t>();
+                a.stab_mask = buckets - 1;
+            }
         }
+        h->start_bound = 0;
         HIPCHK(hipEventRecord(h->ev[2], s));
         launch_walk(a, true, s);
         HIPCHK(hipGetLastError());
@@ -674,6 +693,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         }
         h->grown = grow;
         h->scratch.ensure(std::max<uint64_t>(saved, 1) * 4);
+        h->start_bound = saved + (insert ? total_chg : 0);   // the sources' degrees after the update, at most
         const uint32_t rs = (uint32_t)h->rec_stride();
         launch_save_rows(h->runs.as<RunInfo>(), k, h->adj.as<uint32_t>(), sofs, h->scratch.as<uint32_t>(), s);
         launch_merge_rows(h->runs.as<RunInfo>(), k, bkeys, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(),
@@ -1267,7 +1287,8 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->erec2.cap + h->scratch.cap + h->rplan.cap + h->pscan.cap;
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
                       h->runs.cap + h->fplan.cap + h->memo.cap + h->srcidx.cap + h->count.cap + h->pairs.cap +
-                      h->sel.cap + h->defer.cap + h->rtab.cap + h->bitmap.cap + h->counters.cap + h->errflag.cap;
+                      h->sel.cap + h->defer.cap + h->stab.cap + h->rtab.cap + h->bitmap.cap + h->counters.cap +
+                      h->errflag.cap;
     r.total_bytes = r.csr_bytes + r.records_bytes + r.walks_bytes + r.samplers_bytes + r.edge_hash_bytes +
                     r.update_buffers_bytes + r.scratch_bytes;
     *out = r;

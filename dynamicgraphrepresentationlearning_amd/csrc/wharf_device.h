@@ -36,7 +36,15 @@ __host__ __device__ __forceinline__ uint32_t row_cap_grown(uint32_t d) { return 
 // the product's top bits, the two bit positions from bits 8-12 and 13-17.
 __device__ __forceinline__ uint32_t bloom_mix(uint32_t x) { return __umul24(x ^ (x >> 15), 0x9E3779u); }
 __device__ __forceinline__ uint32_t bloom_word(uint32_t h) { return h >> 20; }
-__device__ __forceinline__ uint32_t bloom_bits(uint32_t h) { return (1u << ((h >> 13) & 31u)) | (1u << ((h >> 8) & 31u)); }
+#ifndef WHARF_BLOOM_K
+#define WHARF_BLOOM_K 3   // bits per key, the third from bits 3-7 (2: scan 3.2-3.4 vs 3.2-3.3 ms, profiles/r02/chunked_scan)
+#endif
+__device__ __forceinline__ uint32_t bloom_bits(uint32_t h)
+{
+    uint32_t b = (1u << ((h >> 13) & 31u)) | (1u << ((h >> 8) & 31u));
+    if (WHARF_BLOOM_K > 2) b |= 1u << ((h >> 3) & 31u);
+    return b;
+}
 __device__ __forceinline__ bool bloom_test(const uint32_t* f, uint32_t x)
 {
     const uint32_t h = bloom_mix(x), b = bloom_bits(h);
@@ -74,6 +82,7 @@ constexpr uint64_t kOffBits = 40;
 constexpr uint64_t kOffMask = (1ull << kOffBits) - 1;
 constexpr uint32_t kEpochBits = 64 - kOffBits;   // row epoch: the record's top 24 bits
 constexpr uint64_t kAnchorNone64 = ~0ull;
+constexpr uint64_t kStabEmpty = ~0ull;         // re-walk start table: no key (its entries start as kAnchorNone64)
 constexpr uint64_t kAnchorStride = 4;         // u64 words between anchor entries (32-B node2vec edge records)
 constexpr uint64_t kEmptyKey = ~0ull;         // empty slot of the edge hash set
 constexpr uint64_t kTombKey = ~0ull - 1;      // deleted edge (probing continues past it)

@@ -43,6 +43,8 @@ struct WalkArgs {
     int model, init, det;
     int scan_only;               // re-walk: only find rewalk points (apply_walk_updates=false)
     uint64_t* defer;             // node2vec re-walk list {li | p << 56}, tickets << 40 | count in counters[2]
+    uint64_t* stab;              // node2vec MH re-walk: start-state table, buckets of 4 {key, anchor entry}, or null
+    uint64_t stab_mask;          //   buckets - 1
     // deterministic re-walk by suffix table (k_det_suffix + k_rewalk_chunked<true>), or memo == null
     uint32_t* memo;              // [wpv][k][memo_stride]: walk from batch source i in round r, new graph
     const uint32_t* src_idx;     // [n]: index of a batch source in the run table (read for sources only)

@@ -164,8 +164,8 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
 
 // SamplerManager::find (a copy, so the anchor stays frozen: libcuckoo find()
 // returns by value, cuckoohash_map.hh:596-609).  The anchor of state
-// (cur, prev) is cached on the edge prev->cur the walker just crossed (`ein`,
-// its global CSR slot, or -1), tagged with the epoch it was written in.  The
+// (cur, prev) is cached on the edge prev->cur the walker just crossed (`ac`,
+// that slot's entry, or null), tagged with the epoch it was written in.  The
 // reference keeps the sampler in cur's SamplerManager (wharfmh.h:296-301),
 // which is reset only when cur is a batch source (wharfmh.h:504,539): the
 // anchor stays valid while cur's row is unchanged since the tag (checked here)
@@ -283,11 +283,11 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
 }
 
 // The cached anchor of the walker's state, or need = true (no valid entry).
-__device__ __forceinline__ void anchor_lookup(const WalkArgs& a, const Row& rc, const Row& rp, int64_t ein,
+__device__ __forceinline__ void anchor_lookup(const WalkArgs& a, const Row& rc, const Row& rp, const uint64_t* ac,
                                               uint64_t anc, uint32_t& an, uint32_t& cls, bool& need)
 {
     need = true;
-    if (ein >= 0) {
+    if (ac) {
         const uint32_t tag = (uint32_t)(anc >> 32) & 0x3FFFFFFFu;
         if (anc != kAnchorNone64 && tag >= rc.epoch) {
             need = false;
@@ -298,12 +298,12 @@ __device__ __forceinline__ void anchor_lookup(const WalkArgs& a, const Row& rc, 
 }
 
 // Called by every active lane of the wave together (WEIGHT inits are wave-cooperative).
-__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, int64_t ein,
+__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, uint64_t* ac,
                                                uint64_t anc, uint32_t& cls)
 {
     uint32_t an = 0;
     bool need;
-    anchor_lookup(a, rc, rp, ein, anc, an, cls, need);
+    anchor_lookup(a, rc, rp, ac, anc, an, cls, need);
     if (a.init == kInitWeight) {
         anchor_init_wave(a, need, rc, rp, an, cls);
     } else if (need) {
@@ -312,16 +312,16 @@ __device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc,
 #ifdef WHARF_INIT_STATS
     // A/B probe: inits vs distinct states initialised (the first writer's CAS
     // from the stale entry succeeds; a duplicate finds the value already there)
-    if (need && ein >= 0) {
+    if (need && ac) {
         const uint64_t nv = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
-        unsigned long long* slot = reinterpret_cast<unsigned long long*>(a.anchor + (uint64_t)ein * kAnchorStride);
+        unsigned long long* slot = reinterpret_cast<unsigned long long*>(ac);
         const bool won = atomicCAS(slot, (unsigned long long)anc, (unsigned long long)nv) == (unsigned long long)anc;
         atomicAdd(a.counters + 3, 1ull);
         if (won) atomicAdd(a.counters + 4, 1ull);
     }
     return an;
 #endif
-    if (need && ein >= 0) a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+    if (need && ac) *ac = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     return an;
 }
 
@@ -338,7 +338,8 @@ constexpr uint64_t kRecStride = (MODEL == kNode2Vec && !DET) ? 2 : 1;
 
 struct Walker {
     Row rc, rp;      // rows of the current and previous vertex
-    int64_t ein;     // node2vec MH: slot of the edge prev -> cur, or -1
+    uint64_t* ac;    // node2vec MH: the anchor cache entry of the state (cur, prev) — the entry of the
+                     // edge prev -> cur, or of the re-walk start table — or null
     uint64_t anc;    // node2vec MH: anchor entry of that slot
 };
 
@@ -372,7 +373,7 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
             nx = cand;
         } else {
             uint32_t acls;
-            const uint32_t ai = anchor_get(a, w.rc, w.rp, w.ein, w.anc, acls);
+            const uint32_t ai = anchor_get(a, w.rc, w.rp, w.ac, w.anc, acls);
             bool ok = true;   // proposing the anchor itself is always accepted
             if (ai != ci) {
                 // metropolis_hastings_sampler.h:118-122: accept iff w(a) < w(c) or
@@ -392,7 +393,7 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
                 }
             }
             accepts += ok;
-            w.ein = (int64_t)(w.rc.off + (ok ? ci : ai));
+            w.ac = a.anchor + (w.rc.off + (ok ? ci : ai)) * kAnchorStride;
             if (ok) {
                 nx = cand;
                 w.anc = canc;
@@ -406,6 +407,41 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
     return nx.v;
 }
 
+// Re-walk start states (node2vec MH).  A re-walk starts at a batch source x
+// with the walk's previous vertex prev; the anchor of state (x, prev) is
+// cached on the edge prev -> x, a slot of prev's row found by a binary search
+// (~log2 deg(prev) dependent loads, and prev is degree-biased).  Walks share
+// start states (configs[2]: ~28 M re-walks over far fewer (x, prev) pairs),
+// so the re-walk keeps a per-batch table keyed by (x, prev) whose value is
+// the state's anchor entry: one 64-B bucket read finds it (a CAS claims a
+// new key).  It caches the same pure function of the snapshot as the edge
+// entry (x's row was reset in this epoch, so only this epoch's entries are
+// valid in either place), so the corpus does not change.  Buckets of four
+// {key, entry} pairs, linear probing over kStabProbes buckets; null when
+// they are full (the caller searches prev's row).
+constexpr uint32_t kStabProbes = 4;
+__device__ __forceinline__ uint64_t* stab_entry(const WalkArgs& a, uint32_t x, uint32_t prev)
+{
+    typedef unsigned long long ull;
+    const uint64_t key = ((uint64_t)x << 32) | prev;   // ids < 2^32 - 2: ~0 is no key
+    uint64_t b = edge_hash(key) & a.stab_mask;
+    for (uint32_t probe = 0; probe < kStabProbes; probe++, b = (b + 1) & a.stab_mask) {
+        uint64_t* e = a.stab + b * 8;
+        const ulonglong2 q0 = *reinterpret_cast<const ulonglong2*>(e), q1 = *reinterpret_cast<const ulonglong2*>(e + 2);
+        const ulonglong2 q2 = *reinterpret_cast<const ulonglong2*>(e + 4), q3 = *reinterpret_cast<const ulonglong2*>(e + 6);
+        const uint64_t k[4] = {q0.x, q1.x, q2.x, q3.x};
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            if (k[i] == key) return e + 2 * i + 1;
+            if (k[i] == kStabEmpty) {   // (the read may be stale: the CAS decides)
+                const ull old = atomicCAS(reinterpret_cast<ull*>(e + 2 * i), (ull)kStabEmpty, (ull)key);
+                if (old == kStabEmpty || old == key) return e + 2 * i + 1;
+            }
+        }
+    }
+    return nullptr;
+}
+
 // Walker state at position p of walk wid (cur = its vertex): the rows of cur
 // and prev and, for node2vec MH, the slot of the edge prev -> cur.
 template <int MODEL, bool DET>
@@ -414,7 +450,7 @@ __device__ __forceinline__ void walk_state(const WalkArgs& a, uint32_t cur, uint
 {
     w.rc = load_rec(a.vrec, cur);
     w.rp = w.rc;
-    w.ein = -1;
+    w.ac = nullptr;
     w.anc = kAnchorNone64;
     if constexpr (MODEL == kNode2Vec && !DET) {
         if (p > 0) {
@@ -430,8 +466,14 @@ __device__ __forceinline__ void walk_state(const WalkArgs& a, uint32_t cur, uint
         // skipping the search and initialising instead gives the same corpus but
         // many more inits: configs[2] node2vec re-walk 73 -> 93 ms.)
         if (w.rc.deg) {
-            w.ein = row_find(a.adj, w.rp, w.rc.v);
-            if (w.ein >= 0) w.anc = a.anchor[(uint64_t)w.ein * kAnchorStride];
+            // a re-walk start: the start-state table (one bucket read); otherwise,
+            // or when its neighbourhood is full, the edge prev -> cur in prev's row
+            if (p > 0 && a.stab) w.ac = stab_entry(a, w.rc.v, w.rp.v);
+            if (!w.ac) {
+                const int64_t ein = row_find(a.adj, w.rp, w.rc.v);
+                if (ein >= 0) w.ac = a.anchor + (uint64_t)ein * kAnchorStride;
+            }
+            if (w.ac) w.anc = *w.ac;
         }
     }
 }
@@ -996,13 +1038,19 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, o, 64));
         for (uint32_t pos = first; pos < L; pos++) {
-            if (!(active && pos > p)) continue;
             uint32_t val = kSent;
-            if (w.rc.deg) {
+            if (active && pos > p && w.rc.deg) {
                 val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts);
                 steps++;
             }
-            walks[(uint64_t)pos * W + li] = val;
+            // the lanes are walks scattered over a block (sorted by rewalk point),
+            // so these are partial-line stores: 446 M write requests for 5.3 GB of
+            // values on configs[2] (~12-17 ms of the ~60 ms re-walk: a timing
+            // probe without them).  Non-temporal: -1.7 %.  A compact [L][list]
+            // buffer written in whole rows plus a merge pass that rewrites the
+            // matrix rows whole cost as much (sorted 57 -> 47 ms, merge 9.8 ms;
+            // profiles/r02/n2v_rewalk2)
+            if (active && pos > p) __builtin_nontemporal_store(val, walks + (uint64_t)pos * W + li);
         }
     }
     wave_add(a.counters + 0, steps);

@@ -356,9 +356,11 @@ def test_affected_ids_on_device_match_host_list(W):
 
 
 # (WHARF_N2V_REWALK, WHARF_NO_ROW_SLACK, WHARF_POOL_NO_HEADROOM, neighbour filter, WHARF_NO_MEMO,
-#  WHARF_NO_CHUNKED_SCAN)
-PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0"), "flat/move": ("flat", "1", "0", "noslack", "0", "0"),
-         "sorted/repack": ("sorted", "1", "1", "off", "0", "1"), "flat/slack-repack": ("flat", "0", "1", "on", "1", "1")}
+#  WHARF_NO_CHUNKED_SCAN, node2vec re-walk start-state table: on / off / 2 buckets)
+PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0", "on"),
+         "flat/move": ("flat", "1", "0", "noslack", "0", "0", "off"),
+         "sorted/repack": ("sorted", "1", "1", "off", "0", "1", "tiny"),
+         "flat/slack-repack": ("flat", "0", "1", "on", "1", "1", "on")}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -378,8 +380,13 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     Deterministic re-walks by suffix table (k_rewalk_chunked copy) and by
     walking every suffix (WHARF_NO_MEMO=1, k_rewalk_sweep).  Rewalk points
     alone (apply_walk_updates = false): the chunked scan, or with
-    WHARF_NO_CHUNKED_SCAN=1 the sweep kernels in scan-only mode."""
-    n2v_list, no_slack, no_headroom, filt, no_memo, no_chunked = PATHS[path]
+    WHARF_NO_CHUNKED_SCAN=1 the sweep kernels in scan-only mode.  node2vec
+    re-walk starts find their state's anchor entry in the per-batch start-state
+    table, by the binary search in prev's row (WHARF_NO_START_TABLE=1), or
+    mostly by the search after a 2-bucket table fills up."""
+    n2v_list, no_slack, no_headroom, filt, no_memo, no_chunked, stab = PATHS[path]
+    monkeypatch.setenv("WHARF_NO_START_TABLE", "1" if stab == "off" else "0")
+    monkeypatch.setenv("WHARF_START_TABLE_BUCKETS", "2" if stab == "tiny" else "0")
     monkeypatch.setenv("WHARF_NO_MEMO", no_memo)
     monkeypatch.setenv("WHARF_NO_CHUNKED_SCAN", no_chunked)
     monkeypatch.setenv("WHARF_NO_NEIGHBOUR_FILTER", "1" if filt == "off" else "0")

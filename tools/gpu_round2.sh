@@ -49,6 +49,12 @@ for s in "$@"; do
               lib=""; [ $v = cur ] || lib=tools/ab/lib_$v.so
               step proben2v_$v 300 env WHARF_LIB_PATH=$lib python tools/rewalk_probe.py --model node2vec --batches 3
             done ;;
+    pmcn2v) N2V="python3 tools/rewalk_probe.py --model node2vec --batches 2"
+            step pmcn2v_tcc 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_rewalk_sorted|k_rewalk_plan|k_walk" --output-format csv -d gpurun_out/pmcn2v_tcc -o run -- $N2V
+            step pmcn2v_wr 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --kernel-include-regex "k_rewalk_sorted|k_rewalk_sweep|k_walk" --output-format csv -d gpurun_out/pmcn2v_wr -o run -- $N2V
+            step pmcn2v_wsize 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_rewalk_sorted|k_rewalk_sweep|k_walk" --output-format csv -d gpurun_out/pmcn2v_wsize -o run -- $N2V
+            step pmcdw_wr 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --kernel-include-regex "k_rewalk_sorted|k_rewalk_sweep|k_walk" --output-format csv -d gpurun_out/pmcdw_wr -o run -- python3 tools/rewalk_probe.py --batches 2
+            step pmcn2v_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmcn2v_trace -o run -- $N2V ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
