@@ -170,7 +170,7 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
 // which is reset only when cur is a batch source (wharfmh.h:504,539): the
 // anchor stays valid while cur's row is unchanged since the tag (checked here)
 // AND while prev's row is unchanged — the entry sits in prev's row, which a
-// batch rebuilds with empty entries (k_move_edges, k_erec_rows).  That second
+// batch rebuilds with empty entries (k_erec_rows).  That second
 // reset is a deliberate divergence: the reference's surviving
 // sampler was initialised against prev's row as it was at the first visit, a
 // function of which walks visited the state when, which differs per GPU shard;
