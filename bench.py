@@ -459,9 +459,12 @@ def main():
         from dynamicgraphrepresentationlearning_amd.distributed import allgatherv_corpus
         loc = torch.empty((g.number_of_walks, args.length), dtype=torch.int32, device=f"cuda:{dev}")
         g.export_walks_device(loc.data_ptr(), layout="walk")
-        # the whole corpus on every rank, or its first rounds when it would not fit
-        # beside the graph (<= 16 GiB); local rows are round-major
-        rounds = max(1, min(wpv, (16 << 30) // max(n * args.length * 4, 1)))
+        # the whole corpus on every rank (received in place: the output is the
+        # only buffer), or its first rounds when it would not fit in the free
+        # HBM (gloo rehearsal: <= 16 GiB of host memory); local rows are round-major
+        round_bytes = max(n * args.length * 4, 1)
+        room = (16 << 30) if comm_dev == "cpu" else torch.cuda.mem_get_info(dev)[0] - (8 << 30)
+        rounds = max(1, min(wpv, room // round_bytes))
         loc = loc[: (hi - lo) * rounds].to(comm_dev)
         barrier()
         t1 = time.perf_counter()

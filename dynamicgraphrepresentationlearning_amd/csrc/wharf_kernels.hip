@@ -778,7 +778,7 @@ __device__ __forceinline__ XcdRange xcd_range(uint64_t W)
 #endif
 
 template <bool COPY>
-__global__ __launch_bounds__(256) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArgs a)
+__device__ __forceinline__ void rewalk_chunked_body(const WalkArgs& a)
 {
     constexpr uint32_t C = kScanChunk;
     __shared__ uint32_t s_bloom[kBloomWords];
@@ -873,6 +873,29 @@ __global__ __launch_bounds__(256) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArg
         a.aff[li] = (uint8_t)p;
     }
     if (COPY) wave_add(a.counters + 0, steps);
+}
+
+// The scan alone holds no copy state (mv[], the table row): forcing 8 waves per
+// SIMD costs it a few spilled VGPRs and hides more of the bitmap round trips
+// (configs[2] scan 3.36 -> 3.11 ms); the copy spills ~40 VGPRs that way (7.6 ->
+// 15 ms), so it keeps the compiler's choice (profiles/r02/chunked_scan).
+#ifndef WHARF_SCAN_ONLY_WAVES_EU
+#define WHARF_SCAN_ONLY_WAVES_EU 8
+#endif
+#if WHARF_SCAN_ONLY_WAVES_EU
+#define WHARF_SCAN_ONLY_WAVES __attribute__((amdgpu_waves_per_eu(WHARF_SCAN_ONLY_WAVES_EU, WHARF_SCAN_ONLY_WAVES_EU)))
+#else
+#define WHARF_SCAN_ONLY_WAVES WHARF_SCAN_WAVES
+#endif
+template <bool COPY>
+__global__ __launch_bounds__(256) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArgs a)
+{
+    rewalk_chunked_body<COPY>(a);
+}
+template <>
+__global__ __launch_bounds__(256) WHARF_SCAN_ONLY_WAVES void k_rewalk_chunked<false>(WalkArgs a)
+{
+    rewalk_chunked_body<false>(a);
 }
 
 __global__ void k_src_index(const RunInfo* __restrict__ runs, uint64_t k, uint32_t* __restrict__ src_idx)

@@ -40,8 +40,16 @@ def shard_walk_ids(n: int, wpv: int, lo: int, hi: int) -> np.ndarray:
 def allgatherv_corpus(local_walks, shards, n: int, wpv: int, group=None):
     """Reassemble the global corpus [n*wpv, L] (row = walk id) on every rank.
 
-    local_walks: torch tensor [W_local, L] (walk-major, this rank's export order)
-    shards: [(lo, hi)] of every rank.  Returns a tensor on local_walks.device.
+    local_walks: torch tensor [W_local, L] (walk-major, this rank's export
+    order: round-major, rows r*(hi-lo) + (v-lo)).  Returns a tensor on
+    local_walks.device.  Row r*n + v of the output holds walk r*n + v.
+
+    Each round of a peer's shard is a contiguous row block of the output
+    (rows r*n + lo .. r*n + hi), so receives land in place: the only buffer
+    is the output itself (a staging copy of every part would double the
+    footprint — at 8 ranks of weak scaling the whole corpus is 107 GB).  One
+    batch of point-to-point operations per round keeps every peer link busy
+    at once; a round's blocks are hi-lo rows per peer.
     """
     import torch
     import torch.distributed as dist
@@ -49,23 +57,25 @@ def allgatherv_corpus(local_walks, shards, n: int, wpv: int, group=None):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     L = local_walks.shape[1]
-    parts = [torch.empty(((hi - lo) * wpv, L), dtype=local_walks.dtype, device=local_walks.device)
-             for (lo, hi) in shards]
-    parts[rank].copy_(local_walks)
-    ops = []
-    for peer in range(world):
-        if peer == rank:
-            continue
-        if local_walks.numel():
-            ops.append(dist.P2POp(dist.isend, local_walks.contiguous(), peer, group))
-        if parts[peer].numel():
-            ops.append(dist.P2POp(dist.irecv, parts[peer], peer, group))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
-    # scatter the per-rank blocks into walk-id order: row r*n + v
+    lo_r, hi_r = shards[rank]
+    own = hi_r - lo_r
+    if local_walks.shape[0] != own * wpv:
+        raise ValueError(f"rank {rank}: {local_walks.shape[0]} local walks, expected {own} x {wpv} rounds")
+    local_walks = local_walks.contiguous()
     out = torch.empty((n * wpv, L), dtype=local_walks.dtype, device=local_walks.device)
     ov = out.view(wpv, n, L)
-    for (lo, hi), p in zip(shards, parts):
-        ov[:, lo:hi, :] = p.view(wpv, hi - lo, L)
+    ov[:, lo_r:hi_r, :] = local_walks.view(wpv, own, L)
+    for r in range(wpv):
+        ops = []
+        for peer in range(world):
+            if peer == rank:
+                continue
+            lo, hi = shards[peer]
+            if own:
+                ops.append(dist.P2POp(dist.isend, local_walks[r * own:(r + 1) * own], peer, group))
+            if hi > lo:
+                ops.append(dist.P2POp(dist.irecv, ov[r, lo:hi], peer, group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
     return out
