@@ -247,7 +247,12 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
             cv[b] = 0;
             if (t[b] < cnt) {
                 const InitReq q = s_req[wv][t[b]];
+#ifdef WHARF_PROBE_CHEAP_PROPOSAL   // timing probe only: how much of an init is the Philox draw
+                P4 r;
+                r.x0 = (q.cv * 0x9E3779B1u) ^ (q.pv * 0x85EBCA77u) ^ (j[b] * 0xC2B2AE3Du);
+#else
                 const P4 r = philox4x32_10(q.cv, q.pv, j[b], (q.cep << 4) | kStreamAnchor, a.key0, a.key1);
+#endif
                 cv[b] = a.adj[q.coff + pick32(r.x0, q.cdeg)];
             }
         }
