@@ -96,6 +96,7 @@ struct wharf_handle {
     uint64_t fpool_used = 0;                   // words handed out (rows that outgrew theirs leave gaps)
     DevBuf walks, aff, rtab, bitmap, counters, errflag;
     DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, count, pairs, sel, defer, rplan, pscan, scratch;
+    DevBuf preoff;                             // node2vec MH: per-source degree prefix of the anchor pre-init
     DevBuf stab;                               // node2vec MH re-walk: start-state anchor table (k_rewalk_sorted)
     uint64_t start_bound = 0;                  // distinct re-walk start states of the next walk update, at most (0: unknown)
     wharf_stats st{};
@@ -466,7 +467,7 @@ void free_handle(wharf_handle* h)
                       &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->walks, &h->aff, &h->rtab,
                       &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags, &h->chg, &h->cf,
                       &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel, &h->defer, &h->rplan, &h->pscan,
-                      &h->scratch, &h->stab})
+                      &h->scratch, &h->stab, &h->preoff})
         b->release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -553,6 +554,18 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         }
         h->start_bound = 0;
         HIPCHK(hipEventRecord(h->ev[2], s));
+        const char* no_pre = getenv("WHARF_NO_PREINIT");   // A/B and tests: every anchor initialised lazily
+        if (a.model == kNode2Vec && !a.det && a.anchor && !a.scan_only && k && !(no_pre && atoi(no_pre))) {
+            // the batch's invalidated anchors, computed ahead of the re-walk (k_anchor_preinit)
+            h->preoff.ensure((k + 1) * 16);
+            uint64_t* degs = h->preoff.as<uint64_t>();
+            uint64_t* preoff = degs + (k + 1);
+            launch_source_degrees(h->runs.as<RunInfo>(), k, h->vrec.as<ERec>(), degs, s);
+            h->scan_u64(degs, preoff, k + 1);
+            WalkArgs pa = a;
+            pa.runs = h->runs.as<RunInfo>();
+            launch_anchor_preinit(pa, preoff, k, s);
+        }
         launch_walk(a, true, s);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(h->ev[3], s));
@@ -1287,7 +1300,7 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->erec2.cap + h->scratch.cap + h->rplan.cap + h->pscan.cap;
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
                       h->runs.cap + h->fplan.cap + h->memo.cap + h->srcidx.cap + h->count.cap + h->pairs.cap +
-                      h->sel.cap + h->defer.cap + h->stab.cap + h->rtab.cap + h->bitmap.cap + h->counters.cap +
+                      h->sel.cap + h->defer.cap + h->stab.cap + h->preoff.cap + h->rtab.cap + h->bitmap.cap + h->counters.cap +
                       h->errflag.cap;
     r.total_bytes = r.csr_bytes + r.records_bytes + r.walks_bytes + r.samplers_bytes + r.edge_hash_bytes +
                     r.update_buffers_bytes + r.scratch_bytes;

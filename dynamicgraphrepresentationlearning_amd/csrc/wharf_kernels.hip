@@ -247,12 +247,7 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
             cv[b] = 0;
             if (t[b] < cnt) {
                 const InitReq q = s_req[wv][t[b]];
-#ifdef WHARF_PROBE_CHEAP_PROPOSAL   // timing probe only: how much of an init is the Philox draw
-                P4 r;
-                r.x0 = (q.cv * 0x9E3779B1u) ^ (q.pv * 0x85EBCA77u) ^ (j[b] * 0xC2B2AE3Du);
-#else
                 const P4 r = philox4x32_10(q.cv, q.pv, j[b], (q.cep << 4) | kStreamAnchor, a.key0, a.key1);
-#endif
                 cv[b] = a.adj[q.coff + pick32(r.x0, q.cdeg)];
             }
         }
@@ -481,6 +476,80 @@ __device__ __forceinline__ void walk_state(const WalkArgs& a, uint32_t cur, uint
             if (w.ac) w.anc = *w.ac;
         }
     }
+}
+
+// Anchor pre-init after an update batch (node2vec MH).  A batch invalidates
+// the anchors of two families of states around each source x: (y, x) — the
+// entries of x's rebuilt row, slot x -> y — and (x, y) — x's samplers were
+// reset (wharfmh.h:504,539), entries on the in-edges y -> x.  The re-walk
+// visits nearly all of them (configs[2]: ~9.5 M inits per batch, 1.0-1.1 per
+// state), and lazily each init stalls its lock-step wave for three rounds of
+// dependent loads while most lanes have none (~10 ms of a ~58 ms batch).
+// Here one lane per (source, slot) pair computes both states' anchors with
+// every lane of the wave initialising (anchor_init_wave at full occupancy),
+// and writes them where the walkers look: the edge entries, and for (x, y) —
+// the re-walk start states — the start-state table too.  The anchor is a
+// pure function of the snapshot, so the corpus is unchanged (entries the
+// pre-init does not reach, e.g. in-edges of a directed graph without a
+// reverse edge, are initialised lazily as before).
+// preoff[i] = sum of the new degrees of sources < i, preoff[k] = pairs.
+__device__ __forceinline__ void anchor_compute(const WalkArgs& a, bool need, const Row& rc, const Row& rp,
+                                               uint32_t& an, uint32_t& cls)
+{
+    if (a.init == kInitWeight) anchor_init_wave(a, need, rc, rp, an, cls);
+    else if (need) an = anchor_init(a, rc, rp, cls);
+}
+
+__global__ __launch_bounds__(256) void k_anchor_preinit(WalkArgs a, const uint64_t* __restrict__ preoff, uint64_t k)
+{
+    const uint64_t total = preoff[k];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        uint64_t lo = 0, hi = k;   // the source i with preoff[i] <= t < preoff[i + 1]
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (preoff[mid] <= t) lo = mid; else hi = mid;
+        }
+        const uint32_t x = a.runs[lo].src;
+        const Row rx = load_rec(a.vrec, x);
+        const uint64_t e = rx.off + (t - preoff[lo]);
+        const uint32_t y = a.adj[e];
+        const Row ry = load_rec(a.vrec, y);
+        uint32_t an = 0, cls = 0;
+        // (y, x): entry of slot x -> y (a walker that crosses it and stays at y needs y's row)
+        const bool need_a = ry.deg != 0;
+        anchor_compute(a, need_a, ry, rx, an, cls);
+        if (need_a) a.anchor[e * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+        // (x, y): entry of slot y -> x, and the start-state table
+        const int64_t ein = row_find(a.adj, ry, x);
+        const bool need_b = ein >= 0;
+        anchor_compute(a, need_b, rx, ry, an, cls);
+        if (need_b) {
+            const uint64_t v = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+            a.anchor[(uint64_t)ein * kAnchorStride] = v;
+            if (a.stab) {
+                uint64_t* se = stab_entry(a, x, y);
+                if (se) *se = v;
+            }
+        }
+    }
+}
+
+__global__ void k_source_degrees(const RunInfo* __restrict__ runs, uint64_t k, const ERec* __restrict__ vrec,
+                                 uint64_t* __restrict__ out)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= k; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = i < k ? vrec[runs[i].src].deg : 0;
+}
+
+void launch_source_degrees(const RunInfo* runs, uint64_t k, const ERec* vrec, uint64_t* out, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_source_degrees, grid_for(k + 1, 256), 256, 0, s, runs, k, vrec, out);
+}
+
+void launch_anchor_preinit(const WalkArgs& a, const uint64_t* preoff, uint64_t k, hipStream_t s)
+{
+    if (k) hipLaunchKernelGGL(k_anchor_preinit, cu_count() * 8, 256, 0, s, a, preoff, k);
 }
 
 // Generation (wharfmh.h:275-326): every lane of a wave writes the same

@@ -356,11 +356,12 @@ def test_affected_ids_on_device_match_host_list(W):
 
 
 # (WHARF_N2V_REWALK, WHARF_NO_ROW_SLACK, WHARF_POOL_NO_HEADROOM, neighbour filter, WHARF_NO_MEMO,
-#  WHARF_NO_CHUNKED_SCAN, node2vec re-walk start-state table: on / off / 2 buckets)
-PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0", "on"),
-         "flat/move": ("flat", "1", "0", "noslack", "0", "0", "off"),
-         "sorted/repack": ("sorted", "1", "1", "off", "0", "1", "tiny"),
-         "flat/slack-repack": ("flat", "0", "1", "on", "1", "1", "on")}
+#  WHARF_NO_CHUNKED_SCAN, node2vec re-walk start-state table: on / off / 2 buckets, WHARF_NO_PREINIT)
+PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0", "on", "0"),
+         "flat/move": ("flat", "1", "0", "noslack", "0", "0", "off", "0"),
+         "sorted/repack": ("sorted", "1", "1", "off", "0", "1", "tiny", "0"),
+         "flat/slack-repack": ("flat", "0", "1", "on", "1", "1", "on", "0"),
+         "sorted/lazy-inits": ("sorted", "0", "0", "on", "0", "0", "on", "1")}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -383,8 +384,12 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     WHARF_NO_CHUNKED_SCAN=1 the sweep kernels in scan-only mode.  node2vec
     re-walk starts find their state's anchor entry in the per-batch start-state
     table, by the binary search in prev's row (WHARF_NO_START_TABLE=1), or
-    mostly by the search after a 2-bucket table fills up."""
-    n2v_list, no_slack, no_headroom, filt, no_memo, no_chunked, stab = PATHS[path]
+    mostly by the search after a 2-bucket table fills up.  The anchors a batch
+    invalidates are computed ahead of the node2vec re-walk (k_anchor_preinit,
+    into the edge entries and the start-state table) or lazily by the walkers
+    (WHARF_NO_PREINIT=1)."""
+    n2v_list, no_slack, no_headroom, filt, no_memo, no_chunked, stab, no_pre = PATHS[path]
+    monkeypatch.setenv("WHARF_NO_PREINIT", no_pre)
     monkeypatch.setenv("WHARF_NO_START_TABLE", "1" if stab == "off" else "0")
     monkeypatch.setenv("WHARF_START_TABLE_BUCKETS", "2" if stab == "tiny" else "0")
     monkeypatch.setenv("WHARF_NO_MEMO", no_memo)
