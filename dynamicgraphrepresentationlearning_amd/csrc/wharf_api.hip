@@ -43,6 +43,10 @@ struct WharfError : std::runtime_error {
         if (!(cond)) throw WharfError((code), (msg));   \
     } while (0)
 
+struct LastNonzero {   // associative: the scan carries the last nonzero value
+    __host__ __device__ uint32_t operator()(uint32_t x, uint32_t y) const { return y ? y : x; }
+};
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -84,6 +88,7 @@ struct wharf_handle {
     uint64_t n = 0, m = 0, lo = 0, hi = 0, n_loc = 0, W = 0;
     uint32_t L = 0, wpv = 0;
     bool anchors = false, has_walks = false;
+    bool anchors_cold = true;                  // node2vec MH: no generation has filled the anchor cache yet
     uint32_t epoch = 0;
     // slack-row CSR: row v = slots [off[v], off[v] + deg[v]) of the pool (adj, erec), cap[v] reserved
     DevBuf off, adj, deg, cap, vrec, erec, row_epoch, ehash;
@@ -873,6 +878,28 @@ int wharf_generate(wharf_handle* h)
         HIPCHK(hipMemsetAsync(h->counters.p, 0, 16, h->s));
         WalkArgs a = h->walk_args();
         HIPCHK(hipEventRecord(h->ev[0], h->s));
+        // node2vec MH with a cold anchor cache and many more steps than states:
+        // every anchor computed up front (k_anchor_init_all), timed with the generation
+        const char* no_pre = getenv("WHARF_NO_PREINIT");
+        if (a.model == kNode2Vec && !a.det && a.anchor && h->anchors_cold && h->pool_used &&
+            (uint64_t)h->W * (h->L - 1) >= 4 * h->pool_used && !(no_pre && atoi(no_pre))) {
+            size_t free_b = 0, total_b = 0;
+            HIPCHK(hipMemGetInfo(&free_b, &total_b));
+            if (h->pool_used * 4 + (1ull << 30) < free_b) {
+                DevBuf owner;
+                owner.ensure(h->pool_used * 4);
+                uint32_t* ow = owner.as<uint32_t>();
+                HIPCHK(hipMemsetAsync(ow, 0, h->pool_used * 4, h->s));
+                launch_slot_owner_marks(h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->n, ow, h->s);
+                h->rp([&](void* t, size_t& b) {   // last nonzero mark: the owner of every slot
+                    return rocprim::inclusive_scan(t, b, ow, ow, (size_t)h->pool_used, LastNonzero{}, h->s);
+                });
+                launch_anchor_init_all(a, ow, h->pool_used, h->s);
+                HIPCHK(hipStreamSynchronize(h->s));   // before the owner buffer is released
+                owner.release();
+            }
+        }
+        h->anchors_cold = false;
         launch_walk(a, false, h->s);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(h->ev[1], h->s));

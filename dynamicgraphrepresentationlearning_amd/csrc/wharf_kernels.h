@@ -71,6 +71,8 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s);
 void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStream_t s);
 void launch_source_degrees(const RunInfo* runs, uint64_t k, const ERec* vrec, uint64_t* out, hipStream_t s);
 void launch_anchor_preinit(const WalkArgs& a, const uint64_t* preoff, uint64_t k, hipStream_t s);
+void launch_slot_owner_marks(const uint64_t* off, const uint32_t* deg, uint64_t n, uint32_t* owner, hipStream_t s);
+void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t slots, hipStream_t s);
 void launch_vrec(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* row_epoch, ERec* vrec,
                  hipStream_t s);
 void launch_erec(const uint32_t* adj, uint64_t slots, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anchors,

@@ -215,9 +215,11 @@ struct InitReq {     // a lane's init, published for the wave
 // compiler from moving the per-init table accesses across the phases
 __device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_wave_barrier(); }
 
+template <uint32_t ROUNDS = kInitRounds>
 __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, const Row& rp, uint32_t& slot,
                                  uint32_t& cls)
 {
+    constexpr uint32_t kInitRounds = ROUNDS;
     __shared__ InitReq s_req[kWavesPerBlock][64];
     __shared__ uint32_t s_key[kWavesPerBlock][64];
     const uint64_t mask = __ballot(need);
@@ -493,10 +495,13 @@ __device__ __forceinline__ void walk_state(const WalkArgs& a, uint32_t cur, uint
 // pre-init does not reach, e.g. in-edges of a directed graph without a
 // reverse edge, are initialised lazily as before).
 // preoff[i] = sum of the new degrees of sources < i, preoff[k] = pairs.
+#ifndef WHARF_PREINIT_ROUNDS
+#define WHARF_PREINIT_ROUNDS 4   // proposals per lane in flight in the pre-init kernels (full waves)
+#endif
 __device__ __forceinline__ void anchor_compute(const WalkArgs& a, bool need, const Row& rc, const Row& rp,
                                                uint32_t& an, uint32_t& cls)
 {
-    if (a.init == kInitWeight) anchor_init_wave(a, need, rc, rp, an, cls);
+    if (a.init == kInitWeight) anchor_init_wave<WHARF_PREINIT_ROUNDS>(a, need, rc, rp, an, cls);
     else if (need) an = anchor_init(a, rc, rp, cls);
 }
 
@@ -533,6 +538,50 @@ __global__ __launch_bounds__(256) void k_anchor_preinit(WalkArgs a, const uint64
             }
         }
     }
+}
+
+// Generation with a cold anchor cache (node2vec MH, the first generation of a
+// handle): when the walks take many more steps than there are states, nearly
+// every state (cur, prev) — one per CSR slot prev -> cur — is entered, and
+// lazily each first entry stalls its lock-step wave for an init.  Instead the
+// anchors of all slots are computed up front, one lane per slot, every lane of
+// a wave initialising; the same pure function of the snapshot, so the corpus
+// is unchanged.  owner[e] = (row owner of slot e) + 1, from the row starts by
+// a last-nonzero scan (k_slot_owner_marks + the host's scan); slack slots hold
+// kGap and are skipped.
+__global__ void k_slot_owner_marks(const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg, uint64_t n,
+                                   uint32_t* __restrict__ owner)
+{
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
+        if (deg[v]) owner[off[v]] = (uint32_t)v + 1;
+}
+
+__global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint32_t* __restrict__ owner, uint64_t slots)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < slots; e += stride) {
+        const uint32_t y = a.adj[e], o = owner[e];
+        bool need = y != kGap && o != 0;
+        Row rx{}, ry{};
+        if (need) {
+            rx = load_rec(a.vrec, o - 1);
+            ry = load_rec(a.vrec, y);
+            need = e < rx.off + rx.deg && ry.deg != 0;   // (slots past a row's end are kGap; the test is cheap)
+        }
+        uint32_t an = 0, cls = 0;
+        anchor_compute(a, need, ry, rx, an, cls);
+        if (need) a.anchor[e * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+    }
+}
+
+void launch_slot_owner_marks(const uint64_t* off, const uint32_t* deg, uint64_t n, uint32_t* owner, hipStream_t s)
+{
+    if (n) hipLaunchKernelGGL(k_slot_owner_marks, grid_for(n, 256), 256, 0, s, off, deg, n, owner);
+}
+
+void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t slots, hipStream_t s)
+{
+    if (slots) hipLaunchKernelGGL(k_anchor_init_all, cu_count() * 8, 256, 0, s, a, owner, slots);
 }
 
 __global__ void k_source_degrees(const RunInfo* __restrict__ runs, uint64_t k, const ERec* __restrict__ vrec,
