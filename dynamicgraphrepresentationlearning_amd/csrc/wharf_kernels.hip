@@ -485,8 +485,9 @@ __device__ __forceinline__ void walk_state(const WalkArgs& a, uint32_t cur, uint
 // entries of x's rebuilt row, slot x -> y — and (x, y) — x's samplers were
 // reset (wharfmh.h:504,539), entries on the in-edges y -> x.  The re-walk
 // visits nearly all of them (configs[2]: ~9.5 M inits per batch, 1.0-1.1 per
-// state), and lazily each init stalls its lock-step wave for three rounds of
-// dependent loads while most lanes have none (~10 ms of a ~58 ms batch).
+// state), and lazily each init stalls its lock-step wave for rounds of
+// dependent loads while most lanes have none.  Measured on configs[2]: the
+// sorted re-walk 55.8 -> 54.0 ms plus 1.1 ms here (profiles/r02/n2v_preinit).
 // Here one lane per (source, slot) pair computes both states' anchors with
 // every lane of the wave initialising (anchor_init_wave at full occupancy),
 // and writes them where the walkers look: the edge entries, and for (x, y) —
@@ -900,8 +901,17 @@ __device__ __forceinline__ XcdRange xcd_range(uint64_t W)
 #define WHARF_SCAN_WAVES
 #endif
 
+// The scan alone holds no copy state (mv[], the table row): forcing 8 waves per
+// SIMD costs it a few spilled VGPRs and hides more of the bitmap round trips
+// (configs[2] scan 3.3 -> 3.15 ms); the copy keeps the compiler's choice (81
+// VGPRs, 5 waves) — forced to more waves it spills and slows (7.6 -> 15 ms),
+// and even the same kernel body moved into a device function compiles to 100
+// VGPRs and runs 25 % slower (profiles/r02/scan_waves).
+#ifndef WHARF_SCAN_ONLY_WAVES_EU
+#define WHARF_SCAN_ONLY_WAVES_EU 8
+#endif
 template <bool COPY>
-__device__ __forceinline__ void rewalk_chunked_body(const WalkArgs& a)
+__global__ __launch_bounds__(256, COPY ? 1 : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArgs a)
 {
     constexpr uint32_t C = kScanChunk;
     __shared__ uint32_t s_bloom[kBloomWords];
@@ -996,29 +1006,6 @@ __device__ __forceinline__ void rewalk_chunked_body(const WalkArgs& a)
         a.aff[li] = (uint8_t)p;
     }
     if (COPY) wave_add(a.counters + 0, steps);
-}
-
-// The scan alone holds no copy state (mv[], the table row): forcing 8 waves per
-// SIMD costs it a few spilled VGPRs and hides more of the bitmap round trips
-// (configs[2] scan 3.36 -> 3.11 ms); the copy spills ~40 VGPRs that way (7.6 ->
-// 15 ms), so it keeps the compiler's choice (profiles/r02/chunked_scan).
-#ifndef WHARF_SCAN_ONLY_WAVES_EU
-#define WHARF_SCAN_ONLY_WAVES_EU 8
-#endif
-#if WHARF_SCAN_ONLY_WAVES_EU
-#define WHARF_SCAN_ONLY_WAVES __attribute__((amdgpu_waves_per_eu(WHARF_SCAN_ONLY_WAVES_EU, WHARF_SCAN_ONLY_WAVES_EU)))
-#else
-#define WHARF_SCAN_ONLY_WAVES WHARF_SCAN_WAVES
-#endif
-template <bool COPY>
-__global__ __launch_bounds__(256) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArgs a)
-{
-    rewalk_chunked_body<COPY>(a);
-}
-template <>
-__global__ __launch_bounds__(256) WHARF_SCAN_ONLY_WAVES void k_rewalk_chunked<false>(WalkArgs a)
-{
-    rewalk_chunked_body<false>(a);
 }
 
 __global__ void k_src_index(const RunInfo* __restrict__ runs, uint64_t k, uint32_t* __restrict__ src_idx)
