@@ -519,6 +519,11 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         HIPCHK(hipMemsetAsync(h->counters.p, 0, 24, s));
         WalkArgs a = h->walk_args();
         a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
+        // chunked scans: non-temporal row loads when most walks are expected to re-walk.  The
+        // share grows with k * L / n (RMAT batches: configs[2] 0.19 -> 81 % re-walk, NT loads
+        // win; configs[3] 1/8 shard 0.024 -> 32 %, they lose 35 %); WHARF_NT_ROWS=0/1 forces it
+        const char* ntr = getenv("WHARF_NT_ROWS");
+        a.nt_rows = ntr ? (atoi(ntr) != 0) : ((double)k * h->L >= 0.08 * (double)std::max<uint64_t>(h->n, 1));
         // deterministic mode: suffixes walked once per (round, batch source) and copied
         // (k_det_suffix + k_rewalk_chunked<true>) while the table stays small; WHARF_NO_MEMO=1 (tests)
         // re-walks every suffix (k_rewalk_sweep)

@@ -53,6 +53,7 @@ struct WalkArgs {
     uint32_t memo_stride;        // L rounded up to 4 (16-B aligned rows)
                                  // (the table has kMemoPad readable words on either side)
     uint32_t wpv;
+    int nt_rows;                 // chunked scans: non-temporal walk-matrix row loads (most walks re-walk)
 };
 
 

@@ -769,14 +769,19 @@ __global__ __launch_bounds__(256) void k_det_suffix(WalkArgs a)
 #ifndef WHARF_CHUNK_NT
 #define WHARF_CHUNK_NT 3   // bit 0: non-temporal walk loads, bit 1: stores (A/B: -2..-3 % on the copy)
 #endif
+// Non-temporal row loads pay when most walks re-walk (configs[2], 81 %: copy
+// 7.9 -> 7.3 ms, scan 3.25 -> 3.14 ms) and cost when few do (configs[3] 1/8
+// shard, 32 %: copy 7.8 -> 10.7 ms), so the chunked scans are instantiated both
+// ways and the host picks per batch (WalkArgs::nt_rows; profiles/r02/nt_rows).
 constexpr uint32_t kScanChunk = WHARF_SCAN_CHUNK;
 #ifndef WHARF_COPY_GROUP
 #define WHARF_COPY_GROUP 64   // lanes whose row segment the suffix copy writes together
 #endif
 constexpr uint32_t kCopyGroup = WHARF_COPY_GROUP;
+template <bool NTL = (WHARF_CHUNK_NT & 1) != 0>
 __device__ __forceinline__ uint32_t walk_load(const uint32_t* p)
 {
-    if (WHARF_CHUNK_NT & 1) return __builtin_nontemporal_load(p);
+    if (NTL) return __builtin_nontemporal_load(p);
     return *p;
 }
 __device__ __forceinline__ void walk_store(uint32_t* p, uint32_t v)
@@ -792,11 +797,12 @@ __device__ __forceinline__ void walk_store(uint32_t* p, uint32_t v)
 #define WHARF_ROW_BUFFER 0   // A/B (profiles/r02/chunked_scan): same scan time, copy 1-3 % slower
 #endif
 constexpr int kRowRsrcFlags = 0x00020000;   // gfx9 buffer descriptor word 3 (32-bit raw access)
+template <bool NTL = (WHARF_CHUNK_NT & 1) != 0>
 __device__ __forceinline__ uint32_t row_load(const uint32_t* row, uint32_t lane)
 {
-    if (!WHARF_ROW_BUFFER) return walk_load(row + lane);
+    if (!WHARF_ROW_BUFFER) return walk_load<NTL>(row + lane);
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)row, 0, 0x7FFFFFFF, kRowRsrcFlags);
-    return __builtin_amdgcn_raw_buffer_load_b32(r, lane * 4, 0, (WHARF_CHUNK_NT & 1) ? 2 : 0);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, lane * 4, 0, NTL ? 2 : 0);
 }
 __device__ __forceinline__ void row_store(uint32_t* row, uint32_t lane, uint32_t v)
 {
@@ -910,7 +916,7 @@ __device__ __forceinline__ XcdRange xcd_range(uint64_t W)
 #ifndef WHARF_SCAN_ONLY_WAVES_EU
 #define WHARF_SCAN_ONLY_WAVES_EU 8
 #endif
-template <bool COPY>
+template <bool COPY, bool NTL>
 __global__ __launch_bounds__(256, COPY ? 1 : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArgs a)
 {
     constexpr uint32_t C = kScanChunk;
@@ -932,7 +938,7 @@ __global__ __launch_bounds__(256, COPY ? 1 : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCA
         uint32_t* __restrict__ wb = walks + uniform64(li - lane);
         uint32_t cur[C], nxt[C];
 #pragma unroll
-        for (uint32_t j = 0; j < C; j++) cur[j] = j < L ? row_load(wb + (uint64_t)j * W, lane) : kSent;
+        for (uint32_t j = 0; j < C; j++) cur[j] = j < L ? row_load<NTL>(wb + (uint64_t)j * W, lane) : kSent;
         for (uint32_t c0 = 0; c0 < L; c0 += C) {
             const uint32_t cnt = min(C, L - c0);
             const bool was_scanning = scanning;
@@ -944,7 +950,7 @@ __global__ __launch_bounds__(256, COPY ? 1 : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCA
                 // are waited for (loads complete in order: the wait leaves them in flight)
 #pragma unroll
                 for (uint32_t j = 0; j < C; j++)
-                    nxt[j] = c0 + C + j < L ? row_load(wb + (uint64_t)(c0 + C + j) * W, lane) : kSent;
+                    nxt[j] = c0 + C + j < L ? row_load<NTL>(wb + (uint64_t)(c0 + C + j) * W, lane) : kSent;
             }
             if (scanning) {
                 bool ended = false;
@@ -976,7 +982,7 @@ __global__ __launch_bounds__(256, COPY ? 1 : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCA
             if (COPY && more && scanning) {
 #pragma unroll
                 for (uint32_t j = 0; j < C; j++)
-                    nxt[j] = c0 + C + j < L ? row_load(wb + (uint64_t)(c0 + C + j) * W, lane) : kSent;
+                    nxt[j] = c0 + C + j < L ? row_load<NTL>(wb + (uint64_t)(c0 + C + j) * W, lane) : kSent;
             }
             if (COPY) {
 #pragma unroll
@@ -1309,11 +1315,13 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
     const bool chunked = !(nc && atoi(nc));
     if (rewalk && a.det && a.memo && !a.scan_only) {
         hipLaunchKernelGGL(k_det_suffix, grid_for((uint64_t)a.wpv * a.memo_k, 256), 256, 0, s, a);
-        hipLaunchKernelGGL(k_rewalk_chunked<true>, mgrid, block, 0, s, a);
+        if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<true, true>), mgrid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_rewalk_chunked<true, false>), mgrid, block, 0, s, a);
         return;
     }
     if (rewalk && a.scan_only && chunked) {
-        hipLaunchKernelGGL(k_rewalk_chunked<false>, mgrid, block, 0, s, a);
+        if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<false, true>), mgrid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_rewalk_chunked<false, false>), mgrid, block, 0, s, a);
         return;
     }
     if (a.det) WHARF_LAUNCH(kDeepWalk, true);

@@ -356,12 +356,14 @@ def test_affected_ids_on_device_match_host_list(W):
 
 
 # (WHARF_N2V_REWALK, WHARF_NO_ROW_SLACK, WHARF_POOL_NO_HEADROOM, neighbour filter, WHARF_NO_MEMO,
-#  WHARF_NO_CHUNKED_SCAN, node2vec re-walk start-state table: on / off / 2 buckets, WHARF_NO_PREINIT)
-PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0", "on", "0"),
-         "flat/move": ("flat", "1", "0", "noslack", "0", "0", "off", "0"),
-         "sorted/repack": ("sorted", "1", "1", "off", "0", "1", "tiny", "0"),
-         "flat/slack-repack": ("flat", "0", "1", "on", "1", "1", "on", "0"),
-         "sorted/lazy-inits": ("sorted", "0", "0", "on", "0", "0", "on", "1")}
+#  WHARF_NO_CHUNKED_SCAN, node2vec re-walk start-state table: on / off / 2 buckets, WHARF_NO_PREINIT,
+#  WHARF_NT_ROWS: chunked scans with non-temporal or plain row loads)
+PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0", "on", "0", "1"),
+         "flat/move": ("flat", "1", "0", "noslack", "0", "0", "off", "0", "0"),
+         "sorted/repack": ("sorted", "1", "1", "off", "0", "1", "tiny", "0", "1"),
+         "flat/slack-repack": ("flat", "0", "1", "on", "1", "1", "on", "0", "0"),
+         "sorted/lazy-inits": ("sorted", "0", "0", "on", "0", "0", "on", "1", "1"),
+         "sorted/plain-rows": ("sorted", "0", "0", "on", "0", "0", "on", "1", "0")}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -387,8 +389,10 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     mostly by the search after a 2-bucket table fills up.  The anchors a batch
     invalidates are computed ahead of the node2vec re-walk (k_anchor_preinit,
     into the edge entries and the start-state table) or lazily by the walkers
-    (WHARF_NO_PREINIT=1)."""
-    n2v_list, no_slack, no_headroom, filt, no_memo, no_chunked, stab, no_pre = PATHS[path]
+    (WHARF_NO_PREINIT=1).  The chunked scans run with non-temporal and with
+    plain walk-matrix row loads (WHARF_NT_ROWS; the host picks per batch)."""
+    n2v_list, no_slack, no_headroom, filt, no_memo, no_chunked, stab, no_pre, nt_rows = PATHS[path]
+    monkeypatch.setenv("WHARF_NT_ROWS", nt_rows)
     monkeypatch.setenv("WHARF_NO_PREINIT", no_pre)
     monkeypatch.setenv("WHARF_NO_START_TABLE", "1" if stab == "off" else "0")
     monkeypatch.setenv("WHARF_START_TABLE_BUCKETS", "2" if stab == "tiny" else "0")

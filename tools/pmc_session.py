@@ -54,8 +54,8 @@ def main():
         # node2vec: the first launch also fills the anchor cache; warm launches only
         "r02_gen_node2vec_mh_s22": summary("k_walk<1, false>", gf, gw, tr, skip=1, dur_slice=slice(1, 4)),
         "r02_streaming_s22": {
-            "rewalk_point_scan": summary("k_rewalk_chunked<false>", sf, sw, tr),
-            "deterministic_rewalk_copy": summary("k_rewalk_chunked<true>", sf, sw, tr),
+            "rewalk_point_scan": summary("k_rewalk_chunked<false", sf, sw, tr),
+            "deterministic_rewalk_copy": summary("k_rewalk_chunked<true", sf, sw, tr),
             "in_edge_scan": summary("k_patch_in_edges", sf, sw, tr),
             "note": "configs[2] deterministic stream (bench.py --det-rewalk-batches 3 for the PMC passes; "
                     "the default bench under --kernel-trace for durations)"},
