@@ -564,8 +564,14 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         }
         h->start_bound = 0;
         HIPCHK(hipEventRecord(h->ev[2], s));
-        const char* no_pre = getenv("WHARF_NO_PREINIT");   // A/B and tests: every anchor initialised lazily
-        if (a.model == kNode2Vec && !a.det && a.anchor && !a.scan_only && k && !(no_pre && atoi(no_pre))) {
+        // Pre-init pays when this handle's walks enter nearly every state around the sources (the
+        // same test as the cold-cache pass: >= 4 steps per slot; configs[2]: 39).  Its cost does not
+        // shrink with the walk shard, so with few walks per slot (configs[4] 1/8 shard, wpv 1: 0.19)
+        // the lazy inits are cheaper.  WHARF_NO_PREINIT=1 / 0 forces it off / on (A/B and tests).
+        const char* no_pre = getenv("WHARF_NO_PREINIT");
+        const bool dense = (uint64_t)h->W * (h->L - 1) >= 4 * h->pool_used;
+        const bool preinit = no_pre && *no_pre ? atoi(no_pre) == 0 : dense;
+        if (a.model == kNode2Vec && !a.det && a.anchor && !a.scan_only && k && preinit) {
             // the batch's invalidated anchors, computed ahead of the re-walk (k_anchor_preinit)
             h->preoff.ensure((k + 1) * 16);
             uint64_t* degs = h->preoff.as<uint64_t>();
