@@ -1859,8 +1859,12 @@ __device__ __forceinline__ void patch_slot(uint32_t t, uint64_t e, const uint32_
     if (t != kGap && ((bitmap[t >> 5] >> (t & 31)) & 1u)) erec[e * rs] = vrec[t];
 }
 
-// 1024-thread workgroups, two per CU (the 64-KiB filter in LDS), 32 waves per CU
-__global__ __launch_bounds__(1024) void k_patch_in_edges(const uint32_t* __restrict__ adj, uint64_t slots,
+// 1024-thread workgroups, two per CU (the 64-KiB filter in LDS), 32 waves per CU (8 per SIMD: 64 VGPRs)
+#ifndef WHARF_INEDGE_LOADS
+#define WHARF_INEDGE_LOADS 4
+#endif
+constexpr uint32_t kInEdgeLoads = WHARF_INEDGE_LOADS;
+__global__ __launch_bounds__(1024, 8) void k_patch_in_edges(const uint32_t* __restrict__ adj, uint64_t slots,
                                                         const uint32_t* __restrict__ bitmap,
                                                         const uint32_t* __restrict__ bloom_big,
                                                         const ERec* __restrict__ vrec, ERec* __restrict__ erec,
@@ -1874,14 +1878,26 @@ __global__ __launch_bounds__(1024) void k_patch_in_edges(const uint32_t* __restr
     const uint64_t n4 = slots / 4, stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const u32x4* __restrict__ a4 = reinterpret_cast<const u32x4*>(adj);
-    for (uint64_t q = g; q < n4; q += stride) {
-        const u32x4 t = __builtin_nontemporal_load(a4 + q);
-        // Bloom-test the four slots branch-free (kGap may pass: the exact test rejects it)
-        const uint32_t hit = (uint32_t)bloom_test_big(s_bloom, t.x) | (uint32_t)bloom_test_big(s_bloom, t.y) << 1 |
-                             (uint32_t)bloom_test_big(s_bloom, t.z) << 2 | (uint32_t)bloom_test_big(s_bloom, t.w) << 3;
-        if (hit) {
-            for (uint32_t j = 0; j < 4; j++)
-                if ((hit >> j) & 1u) patch_slot(t[j], 4 * q + j, bitmap, vrec, erec, rs);
+    // kInEdgeLoads 16-B loads per thread in flight (one left the pass latency-bound at 8 MB in flight;
+    // configs[3] pool, 10.2 GB: 1 / 2 / 4 loads 3.00 / 2.75 / 2.65 ms, profiles/r02/in_edge_scan)
+    for (uint64_t q0 = g; q0 < n4; q0 += kInEdgeLoads * stride) {
+        u32x4 tv[kInEdgeLoads];
+#pragma unroll
+        for (uint32_t u = 0; u < kInEdgeLoads; u++) {
+            const uint64_t q = q0 + u * stride;
+            tv[u] = q < n4 ? __builtin_nontemporal_load(a4 + q) : u32x4{kGap, kGap, kGap, kGap};
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kInEdgeLoads; u++) {
+            const u32x4 t = tv[u];
+            // Bloom-test the four slots branch-free (kGap may pass: the exact test rejects it)
+            const uint32_t hit = (uint32_t)bloom_test_big(s_bloom, t.x) | (uint32_t)bloom_test_big(s_bloom, t.y) << 1 |
+                                 (uint32_t)bloom_test_big(s_bloom, t.z) << 2 | (uint32_t)bloom_test_big(s_bloom, t.w) << 3;
+            if (hit) {
+                const uint64_t q = q0 + u * stride;
+                for (uint32_t j = 0; j < 4; j++)
+                    if ((hit >> j) & 1u) patch_slot(t[j], 4 * q + j, bitmap, vrec, erec, rs);
+            }
         }
     }
     if (g < slots - 4 * n4) {   // the pool's last < 4 slots
