@@ -22,6 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # WHARF_LIB_PATH: an alternative build of the same library (A/B experiments in tools/)
 LIB_PATH = os.environ.get("WHARF_LIB_PATH") or os.path.join(_HERE, "libwharf_gpu.so")
 
+ABI_VERSION = 4   # WHARF_ABI_VERSION of include/wharf_gpu.h
 WHARF_OK = 0
 WHARF_DEEPWALK, WHARF_NODE2VEC = 0, 1
 WHARF_INIT_RANDOM, WHARF_INIT_BURNIN, WHARF_INIT_WEIGHT = 0, 1, 2
@@ -65,6 +66,9 @@ class wharf_stats(C.Structure):
         ("pool_capacity", C.c_uint64),
         ("last_moved_row_slots", C.c_uint64),
         ("repacks", C.c_uint64),
+        ("dead_slots", C.c_uint64),
+        ("last_anchor_inits", C.c_uint64),
+        ("last_rewalk_passes", C.c_uint64),
     ]
 
 
@@ -125,6 +129,12 @@ def load(path: str = LIB_PATH):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+    # the structs above mirror include/wharf_gpu.h of this ABI version: a library
+    # of another version (an A/B build through WHARF_LIB_PATH) would write a
+    # wharf_stats of another size into the ctypes buffer
+    ver = lib.wharf_abi_version()
+    if ver != ABI_VERSION:
+        raise ImportError(f"{path}: WHARF_ABI_VERSION {ver}, this binding expects {ABI_VERSION}; rebuild the library")
     return lib
 
 

@@ -95,6 +95,7 @@ struct wharf_handle {
     DevBuf off2, adj2, erec2;                  // temporaries: contiguous CSR at creation, repack, export
     uint64_t pool_used = 0, pool_cap = 0;      // slots handed out / allocated
     uint64_t repacks = 0, grown = 0;           // pool repacks so far; slots handed to rows moved by the last batch
+    uint64_t dead_slots = 0;                   // old places of moved rows (kGap) until a repack / compaction
     uint64_t ehash_mask = 0, ehash_used = 0;   // capacity - 1; occupied slots incl. tombstones
     DevBuf fdir, fpool, fplan;                 // node2vec MH: per-row neighbour filters (k_filter_*)
     DevBuf memo, srcidx;                       // deterministic re-walk: suffix table, source index
@@ -103,9 +104,69 @@ struct wharf_handle {
     DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, count, pairs, sel, defer, rplan, pscan, scratch;
     DevBuf preoff;                             // node2vec MH: per-source degree prefix of the anchor pre-init
     DevBuf stab;                               // node2vec MH re-walk: start-state anchor table (k_rewalk_sorted)
+    DevBuf park, parkc;                        // node2vec MH re-walk passes: two parked-walker lists, their counts
+    uint32_t st_park_passes = 0;               // passes of the last re-walk by passes (0: lock-step kernel)
     uint64_t start_bound = 0;                  // distinct re-walk start states of the next walk update, at most (0: unknown)
     wharf_stats st{};
     std::string err;
+
+    // Host snapshot of the walk matrix for walk() / vertex_at_walk(): the
+    // reference's corpus export calls walk(i) once per walk
+    // (vertex-classification.cpp:145-148), which at one kernel + D2H + sync per
+    // call is ~10^4 round trips per 10^4 walks.  Chunks of kSnapWalks walks are
+    // gathered walk-major on the device and copied to pinned host memory on
+    // first use; every change to the walks (walks_version) invalidates them.
+    static constexpr uint64_t kSnapWalks = 1ull << 16;
+    static constexpr size_t kSnapMaxChunks = 256;   // <= 16 GiB of pinned memory at L = 255
+    struct Snap {
+        uint64_t chunk = ~0ull;
+        uint32_t* host = nullptr;
+    };
+    uint64_t walks_version = 0, snap_version = ~0ull;
+    std::vector<Snap> snaps;
+    std::vector<int64_t> snap_of;   // chunk -> slot in snaps, or -1
+    size_t snap_next = 0;
+
+    void walks_changed() { walks_version++; }
+
+    // walk-major row (L entries) of owned walk li, from the snapshot
+    const uint32_t* snap_row(uint64_t li)
+    {
+        const uint64_t nchunks = (W + kSnapWalks - 1) / kSnapWalks, c = li / kSnapWalks;
+        if (snap_version != walks_version || snap_of.size() != nchunks) {
+            snap_of.assign(nchunks, -1);
+            for (Snap& x : snaps) x.chunk = ~0ull;
+            snap_version = walks_version;
+        }
+        if (snap_of[c] < 0) {
+            size_t slot;
+            if (snaps.size() < kSnapMaxChunks) {
+                snaps.emplace_back();
+                slot = snaps.size() - 1;
+                HIPCHK(hipHostMalloc((void**)&snaps[slot].host, kSnapWalks * L * 4, hipHostMallocDefault));
+            } else {
+                slot = snap_next;
+                snap_next = (snap_next + 1) % kSnapMaxChunks;
+                if (snaps[slot].chunk != ~0ull) snap_of[snaps[slot].chunk] = -1;
+            }
+            const uint64_t base = c * kSnapWalks, cnt = std::min(kSnapWalks, W - base);
+            sel.ensure(kSnapWalks * L * 4);
+            launch_gather_rows(walks.as<uint32_t>(), W, L, nullptr, base, cnt, sel.as<uint32_t>(), s);
+            HIPCHK(hipMemcpyAsync(snaps[slot].host, sel.p, cnt * L * 4, hipMemcpyDeviceToHost, s));
+            sync();
+            snaps[slot].chunk = c;
+            snap_of[c] = (int64_t)slot;
+        }
+        return snaps[snap_of[c]].host + (li - c * kSnapWalks) * L;
+    }
+    void free_snaps()
+    {
+        for (Snap& x : snaps)
+            if (x.host) (void)hipHostFree(x.host);
+        snaps.clear();
+        snap_of.clear();
+        snap_next = 0;
+    }
 
     void sync() { HIPCHK(hipStreamSynchronize(s)); }
     uint64_t bitmap_words() const { return (((n + 31) / 32 + 1) + 3) & ~3ull; }   // the filters after it stay 16-B aligned
@@ -146,10 +207,13 @@ struct wharf_handle {
     // slots the pool holds for `used` handed-out slots: 1/16 headroom (rows that
     // outgrow their slack move to its end) plus `extra`; none with
     // WHARF_POOL_NO_HEADROOM=1 (tests: every moved row repacks the pool)
+    // (WHARF_POOL_HEADROOM=<slots>, tests: exactly that headroom)
     static uint64_t pool_capacity(uint64_t used, uint64_t extra)
     {
         const char* nh = getenv("WHARF_POOL_NO_HEADROOM");
-        const uint64_t head = nh && atoi(nh) ? 0 : std::max<uint64_t>(used >> 4, 1ull << 16);
+        const char* hs = getenv("WHARF_POOL_HEADROOM");
+        uint64_t head = nh && atoi(nh) ? 0 : std::max<uint64_t>(used >> 4, 1ull << 16);
+        if (hs && *hs && !(nh && atoi(nh))) head = strtoull(hs, nullptr, 10);
         return used + head + extra;
     }
     // WHARF_NO_ROW_SLACK=1 (tests): rows get no slack, so every growing row moves
@@ -196,36 +260,140 @@ struct wharf_handle {
                          adj.as<uint32_t>(), nullptr, nullptr, s);
     }
 
+    // Device bytes still available (WHARF_REPACK_MEM_CAP=<bytes>, tests: as if only that much were free)
+    static uint64_t free_bytes()
+    {
+        size_t f = 0, t = 0;
+        HIPCHK(hipMemGetInfo(&f, &t));
+        const char* c = getenv("WHARF_REPACK_MEM_CAP");
+        return c ? std::min<uint64_t>(f, strtoull(c, nullptr, 10)) : (uint64_t)f;
+    }
+
+    // Room for `extra` more slots in the pool: a repack into a second pool with
+    // fresh slack when the device can hold both pools, else the in-place
+    // compaction (no second pool: dead slots squeezed out, capacities kept).
+    // Neither changes what the handle computes, only where rows live.
+    void make_room(uint64_t extra)
+    {
+        const uint64_t pc = pool_capacity(pool_used, extra);
+        const uint64_t need = pc * (4 + sizeof(ERec) * rec_stride()) + 3 * (n + 1) * 8 + (256ull << 20);
+        if (need <= free_bytes()) repack(extra);
+        else compact();
+    }
+
     // Fresh slack for every row, in a new pool with room for `extra` more slots
     // (the pool ran out of headroom): rows, their anchor entries and records
-    // move; the records are rebuilt (every row offset changed).
+    // move; the records are rebuilt (every row offset changed).  Nothing of the
+    // handle changes until the new pool is complete: a failed allocation leaves
+    // it as it was.
     void repack(uint64_t extra)
     {
         const uint64_t rs = rec_stride();
-        DevBuf capw;
-        capw.ensure((n + 1) * 8);
-        launch_row_recap(deg.as<uint32_t>(), n, cap.as<uint32_t>(), capw.as<uint64_t>(), row_slack(), s);
-        off2.ensure((n + 1) * 8);
-        scan_u64(capw.as<uint64_t>(), off2.as<uint64_t>(), n + 1);
-        uint64_t used = 0;
-        HIPCHK(hipMemcpyAsync(&used, off2.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
-        sync();
-        capw.release();
-        const uint64_t pc = pool_capacity(used, extra);
-        adj2.ensure(std::max<uint64_t>(pc, 1) * 4);
-        HIPCHK(hipMemsetAsync(adj2.p, 0xFF, std::max<uint64_t>(pc, 1) * 4, s));
-        erec2.ensure(std::max<uint64_t>(pc, 1) * sizeof(ERec) * rs);
-        launch_copy_rows(off.as<uint64_t>(), deg.as<uint32_t>(), adj.as<uint32_t>(), off2.as<uint64_t>(), n,
-                         adj2.as<uint32_t>(), anchors ? erec.as<uint64_t>() + 2 : nullptr,
-                         anchors ? erec2.as<uint64_t>() + 2 : nullptr, s);
-        std::swap(off, off2);
-        std::swap(adj, adj2);
-        std::swap(erec, erec2);
+        DevBuf capw, cap2;
+        try {
+            capw.ensure((n + 1) * 8);
+            cap2.ensure(std::max<uint64_t>(n, 1) * 4);
+            launch_row_recap(deg.as<uint32_t>(), n, cap2.as<uint32_t>(), capw.as<uint64_t>(), row_slack(), s);
+            off2.ensure((n + 1) * 8);
+            scan_u64(capw.as<uint64_t>(), off2.as<uint64_t>(), n + 1);
+            uint64_t used = 0;
+            HIPCHK(hipMemcpyAsync(&used, off2.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+            sync();
+            capw.release();
+            const uint64_t pc = pool_capacity(used, extra);
+            adj2.ensure(std::max<uint64_t>(pc, 1) * 4);
+            HIPCHK(hipMemsetAsync(adj2.p, 0xFF, std::max<uint64_t>(pc, 1) * 4, s));
+            erec2.ensure(std::max<uint64_t>(pc, 1) * sizeof(ERec) * rs);
+            launch_copy_rows(off.as<uint64_t>(), deg.as<uint32_t>(), adj.as<uint32_t>(), off2.as<uint64_t>(), n,
+                             adj2.as<uint32_t>(), anchors ? erec.as<uint64_t>() + 2 : nullptr,
+                             anchors ? erec2.as<uint64_t>() + 2 : nullptr, s);
+            HIPCHK(hipGetLastError());
+            sync();
+            std::swap(off, off2);
+            std::swap(adj, adj2);
+            std::swap(erec, erec2);
+            std::swap(cap, cap2);
+            pool_used = used;
+            pool_cap = pc;
+        } catch (...) {
+            capw.release();
+            cap2.release();
+            off2.release();
+            adj2.release();
+            erec2.release();
+            throw;
+        }
+        cap2.release();
         off2.release();
         adj2.release();
         erec2.release();
-        pool_used = used;
-        pool_cap = pc;
+        dead_slots = 0;
+        launch_vrec(off.as<uint64_t>(), deg.as<uint32_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
+        launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rs, 1, s);
+        repacks++;
+    }
+
+    // In-place compaction (k_compact_gather / k_compact_put): rows in slot
+    // order keep their capacities and close up the dead slots moved rows left,
+    // window by window through a staging buffer of at most half the free
+    // memory.  Needs O(n) scratch instead of a second pool.
+    void compact()
+    {
+        const uint64_t rs = rec_stride();
+        DevBuf keys, vals, keys2, order, capw, snoff, sadj, sanc;
+        try {
+            keys.ensure(std::max<uint64_t>(n, 1) * 8);
+            keys2.ensure(std::max<uint64_t>(n, 1) * 8);
+            vals.ensure(std::max<uint64_t>(n, 1) * 4);
+            order.ensure(std::max<uint64_t>(n, 1) * 4);
+            launch_slot_order_keys(off.as<uint64_t>(), cap.as<uint32_t>(), n, keys.as<uint64_t>(), vals.as<uint32_t>(), s);
+            uint64_t* ki = keys.as<uint64_t>();
+            uint64_t* ko = keys2.as<uint64_t>();
+            uint32_t* vi = vals.as<uint32_t>();
+            uint32_t* vo = order.as<uint32_t>();
+            const unsigned eb = std::max<uint32_t>(bits_for(pool_cap + 1), 1);
+            rp([&](void* t, size_t& b) { return rocprim::radix_sort_pairs(t, b, ki, ko, vi, vo, (size_t)n, 0u, eb, s); });
+            keys.release();
+            keys2.release();
+            vals.release();
+            capw.ensure((n + 1) * 8);
+            snoff.ensure((n + 1) * 8);
+            launch_ordered_caps(order.as<uint32_t>(), cap.as<uint32_t>(), n, capw.as<uint64_t>(), s);
+            scan_u64(capw.as<uint64_t>(), snoff.as<uint64_t>(), n + 1);
+            capw.release();
+            std::vector<uint64_t> hsn(n + 1);
+            HIPCHK(hipMemcpyAsync(hsn.data(), snoff.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+            sync();
+            const uint64_t used = hsn[n];
+            const uint64_t per = 4 + (anchors ? 8 : 0);
+            const uint64_t C = std::max<uint64_t>(std::min<uint64_t>(free_bytes() / 2 / per, used), std::min<uint64_t>(used, 1ull << 20));
+            sadj.ensure(std::max<uint64_t>(C, 1) * 4);
+            if (anchors) sanc.ensure(std::max<uint64_t>(C, 1) * 8);
+            uint64_t* anc = anchors ? erec.as<uint64_t>() + 2 : nullptr;
+            for (uint64_t D = 0; D < used; D += C) {
+                const uint64_t cnt = std::min(C, used - D);
+                HIPCHK(hipMemsetAsync(sadj.p, 0xFF, cnt * 4, s));   // slack slots: kGap
+                if (anchors) HIPCHK(hipMemsetAsync(sanc.p, 0xFF, cnt * 8, s));
+                // rows in slot order whose new places meet [D, D + cnt)
+                const uint64_t r0 = (uint64_t)(std::upper_bound(hsn.begin(), hsn.begin() + n, D) - hsn.begin());
+                const uint64_t r1 = (uint64_t)(std::lower_bound(hsn.begin(), hsn.begin() + n, D + cnt) - hsn.begin());
+                launch_compact_gather(order.as<uint32_t>(), snoff.as<uint64_t>(), r0 ? r0 - 1 : 0, r1,
+                                      off.as<uint64_t>(), deg.as<uint32_t>(), adj.as<uint32_t>(), anc, D, cnt,
+                                      sadj.as<uint32_t>(), anchors ? sanc.as<uint64_t>() : nullptr, s);
+                launch_compact_put(sadj.as<uint32_t>(), anchors ? sanc.as<uint64_t>() : nullptr, cnt, D,
+                                   adj.as<uint32_t>(), anc, s);
+            }
+            if (pool_used > used) HIPCHK(hipMemsetAsync(adj.as<uint32_t>() + used, 0xFF, (pool_used - used) * 4, s));
+            launch_scatter_offsets(order.as<uint32_t>(), snoff.as<uint64_t>(), n, off.as<uint64_t>(), s);
+            HIPCHK(hipGetLastError());
+            sync();
+            pool_used = used;
+        } catch (...) {
+            for (DevBuf* b : {&keys, &vals, &keys2, &order, &capw, &snoff, &sadj, &sanc}) b->release();
+            throw;
+        }
+        for (DevBuf* b : {&order, &snoff, &sadj, &sanc}) b->release();
+        dead_slots = 0;
         launch_vrec(off.as<uint64_t>(), deg.as<uint32_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
         launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rs, 1, s);
         repacks++;
@@ -255,6 +423,7 @@ struct wharf_handle {
         if (walks.p) return;
         walks.ensure(std::max<uint64_t>(W * L, 1) * 4);
         launch_fill_u32(walks.as<uint32_t>(), W * L, kSent, s);
+        walks_changed();
         aff.ensure(std::max<uint64_t>(W, 1));
         has_walks = false;
     }
@@ -375,11 +544,13 @@ struct wharf_handle {
 
     void read_counters()
     {
-        unsigned long long c[7] = {};
-        HIPCHK(hipMemcpyAsync(c, counters.p, 56, hipMemcpyDeviceToHost, s));
+        unsigned long long c[8] = {};
+        HIPCHK(hipMemcpyAsync(c, counters.p, 64, hipMemcpyDeviceToHost, s));
         sync();
         st.steps = c[0];
         st.accepts = c[1];
+        st.last_anchor_inits = c[7];
+        st.last_rewalk_passes = st_park_passes;
 #ifdef WHARF_INIT_STATS
         fprintf(stderr, "[init-stats] epoch %u: steps %llu inits %llu distinct %llu deferred %llu sweep-lane-slots %llu "
                         "list-lane-slots %llu\n", epoch, c[0], c[3], c[4], c[2], c[5], c[6]);
@@ -472,8 +643,9 @@ void free_handle(wharf_handle* h)
                       &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->walks, &h->aff, &h->rtab,
                       &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags, &h->chg, &h->cf,
                       &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel, &h->defer, &h->rplan, &h->pscan,
-                      &h->scratch, &h->stab, &h->preoff})
+                      &h->scratch, &h->stab, &h->preoff, &h->park, &h->parkc})
         b->release();
+    h->free_snaps();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     if (h->s) (void)hipStreamDestroy(h->s);
@@ -508,6 +680,46 @@ void rmat_keys(wharf_handle* h, uint64_t edges_number, uint64_t vertices_number,
     launch_rmat_keys(p, edges_number, directed, h->k1.as<uint64_t>(), h->s);
 }
 
+// node2vec MH re-walk by passes (k_rewalk_park): the walkers of
+// k_rewalk_plan's list advance until they need an anchor that is not cached,
+// the parked states' anchors are computed with full waves, and the next pass
+// resumes them; a short list is finished with in-wave inits.  One sync per pass
+// reads the parked count.
+constexpr uint64_t kParkTail = 8192;   // parked walkers below which the last pass initialises in the wave
+
+void park_passes(wharf_handle* h, const WalkArgs& a)
+{
+    hipStream_t s = h->s;
+    uint64_t c2 = 0;
+    HIPCHK(hipMemcpyAsync(&c2, a.counters + 2, 8, hipMemcpyDeviceToHost, s));
+    h->sync();
+    const uint64_t listn = c2 & kListMask;
+    h->st_park_passes = 0;
+    if (!listn) return;
+    h->park.ensure(2 * listn * kParkRecBytes);
+    h->parkc.ensure(16);
+    unsigned long long* pc = h->parkc.as<unsigned long long>();
+    char* P[2] = {h->park.as<char>(), h->park.as<char>() + listn * kParkRecBytes};
+    HIPCHK(hipMemsetAsync(pc, 0, 16, s));
+    launch_rewalk_park(a, 1, 1, nullptr, nullptr, P[0], pc, s);
+    const char* te = getenv("WHARF_PARK_TAIL");   // tests: 0 = park until no walker is left
+    const uint64_t tail = te ? strtoull(te, nullptr, 10) : kParkTail;
+    uint32_t passes = 1;
+    for (int cur = 0;; cur ^= 1) {
+        uint64_t cnt = 0;
+        HIPCHK(hipMemcpyAsync(&cnt, pc + cur, 8, hipMemcpyDeviceToHost, s));
+        h->sync();
+        if (!cnt) break;
+        launch_park_init(a, P[cur], pc + cur, s);
+        const bool last = cnt < tail;
+        HIPCHK(hipMemsetAsync(pc + (cur ^ 1), 0, 8, s));
+        launch_rewalk_park(a, 0, last ? 0 : 1, P[cur], pc + cur, P[cur ^ 1], pc + (cur ^ 1), s);
+        passes++;
+        if (last) break;
+    }
+    h->st_park_passes = passes;
+}
+
 // Rewalk points + suffix re-walk (wharfmh.h:519-537, batch_walk_update
 // 733-923) of every owned walk that holds a vertex of the bitmap; h->runs
 // holds the k sources (the deterministic suffix table is keyed by them), and
@@ -517,6 +729,8 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
     hipStream_t s = h->s;
     if (h->has_walks && h->W) {
         HIPCHK(hipMemsetAsync(h->counters.p, 0, 24, s));
+        HIPCHK(hipMemsetAsync(h->counters.as<unsigned long long>() + 7, 0, 8, s));
+        h->st_park_passes = 0;
         WalkArgs a = h->walk_args();
         a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
         // chunked scans: non-temporal row loads when most walks are expected to re-walk.  The
@@ -582,8 +796,17 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
             pa.runs = h->runs.as<RunInfo>();
             launch_anchor_preinit(pa, preoff, k, s);
         }
+        // node2vec MH re-walk: by passes with batched anchor inits where the walks are sparse in
+        // the states (the cold-cache case: the pre-init rule's `dense` is false), else the
+        // lock-step sorted kernel.  WHARF_N2V_REWALK=park|sorted|flat forces one.
+        const char* rw = getenv("WHARF_N2V_REWALK");
+        const std::string rmode = rw ? rw : "";
+        a.park = a.model == kNode2Vec && !a.det && a.anchor && !a.scan_only &&
+                 (rmode == "park" || (rmode.empty() && !dense));
+        h->walks_changed();
         launch_walk(a, true, s);
         HIPCHK(hipGetLastError());
+        if (a.park) park_passes(h, a);
         HIPCHK(hipEventRecord(h->ev[3], s));
         // ascending affected walk ids: count per block, scan, write
         const unsigned nb = aff_blocks(h->W);
@@ -627,7 +850,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         auto t0 = std::chrono::steady_clock::now();
         h->st.affected = 0;
         h->st.batch_edges = 0;
-        h->st.steps = h->st.accepts = 0;
+        h->st.steps = h->st.accepts = h->st.last_anchor_inits = h->st.last_rewalk_passes = 0;
         h->st.last_graph_update_ms = h->st.last_walk_update_ms = h->st.last_walk_kernel_ms = 0;
         h->st.last_csr_move_ms = 0;
         h->st.last_moved_slots = 0;
@@ -686,9 +909,11 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         //    or moved to the pool's end; their samplers are reset (row epoch)
         const uint64_t m_new = insert ? h->m + total_chg : h->m - total_chg;
         // row epochs live in 24 bits of the records (wharf_device.h make_rec) and
-        // feed the Philox counters: refuse the batch that would wrap them
+        // feed the Philox counters: refuse the batch that would wrap them.  The
+        // epoch (and the sources' row epochs, k_commit_rows) advance only once
+        // the batch can no longer fail: after the pool planning below.
         REQUIRE(h->epoch + 1 < (1u << kEpochBits), WHARF_E_INVALID, "update epoch limit (2^24 applied batches) reached");
-        h->epoch++;
+        const uint32_t epoch = h->epoch + 1;
         h->runs.ensure(k * sizeof(RunInfo));
         h->rplan.ensure(k * sizeof(RowPlan));
         h->pscan.ensure((k + 1) * 32);
@@ -696,30 +921,39 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         uint64_t* save = need + (k + 1);
         uint64_t* relofs = save + (k + 1);
         uint64_t* sofs = relofs + (k + 1);
+        unsigned long long* dead_d = h->errflag.as<unsigned long long>() + 1;
         const int slack = wharf_handle::row_slack();
+        // the in-edge pass reads dead slots too: past a quarter of the pool, reclaim them
+        if (h->dead_slots * 4 > h->pool_used) h->make_room(0);
         uint64_t grow = 0, saved = 0;
+        unsigned long long dead = 0;
         for (int attempt = 0;; attempt++) {
             HIPCHK(hipMemsetAsync(h->bitmap.p, 0, (h->bitmap_words() + kFilterWords) * 4, s));
+            HIPCHK(hipMemsetAsync(dead_d, 0, 8, s));
             launch_run_info(bkeys, h->runstart.as<uint32_t>(), k, mb, h->off.as<uint64_t>(), h->deg.as<uint32_t>(),
-                            h->runs.as<RunInfo>(), h->bitmap.as<uint32_t>(), h->bitmap.as<uint32_t>() + h->bitmap_words(),
-                            h->row_epoch.as<uint32_t>(), h->epoch, s);
+                            h->runs.as<RunInfo>(), h->bitmap.as<uint32_t>(), h->bitmap.as<uint32_t>() + h->bitmap_words(), s);
             launch_plan_rows(h->runs.as<RunInfo>(), k, h->cap.as<uint32_t>(), h->cf.as<uint32_t>(), insert, slack, need,
-                             save, h->rplan.as<RowPlan>(), s);
+                             save, h->rplan.as<RowPlan>(), dead_d, s);
             h->scan_u64(need, relofs, k + 1);
             h->scan_u64(save, sofs, k + 1);
             HIPCHK(hipMemcpyAsync(&grow, relofs + k, 8, hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(&saved, sofs + k, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(&dead, dead_d, 8, hipMemcpyDeviceToHost, s));
             h->sync();
             if (h->pool_used + grow <= h->pool_cap) break;
-            REQUIRE(attempt == 0, WHARF_E_STATE,
-                    "slot pool exhausted after a repack (used " + std::to_string(h->pool_used) + ", grow " +
-                        std::to_string(grow) + ", capacity " + std::to_string(h->pool_cap) + ")");
-            // out of headroom: fresh slack everywhere, then plan again.  The fresh
-            // capacities can be smaller than the old ones (rows that shrank keep
-            // theirs), so room is made for every source moving with grown slack.
+            REQUIRE(attempt == 0, WHARF_E_NOMEM,
+                    "slot pool exhausted: no device memory for a second pool and the in-place compaction left too "
+                    "little room (used " + std::to_string(h->pool_used) + ", grow " + std::to_string(grow) +
+                        ", capacity " + std::to_string(h->pool_cap) + "); the batch was not applied");
+            // out of headroom: fresh slack everywhere (or dead slots squeezed out),
+            // then plan again.  The fresh capacities can be smaller than the old
+            // ones (rows that shrank keep theirs), so room is made for every
+            // source moving with grown slack.
             const uint64_t all = saved + (insert ? total_chg : 0);
-            h->repack(all + all / 8 + 4 * k);
+            h->make_room(all + all / 8 + 4 * k);
         }
+        h->epoch = epoch;
+        h->dead_slots += dead;
         h->grown = grow;
         h->scratch.ensure(std::max<uint64_t>(saved, 1) * 4);
         h->start_bound = saved + (insert ? total_chg : 0);   // the sources' degrees after the update, at most
@@ -729,7 +963,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
                           h->scratch.as<uint32_t>(), sofs, relofs, h->pool_used, insert, h->rplan.as<RowPlan>(),
                           h->adj.as<uint32_t>(), s);
         launch_commit_rows(h->runs.as<RunInfo>(), k, h->rplan.as<RowPlan>(), h->epoch, h->off.as<uint64_t>(),
-                           h->deg.as<uint32_t>(), h->cap.as<uint32_t>(), h->vrec.as<ERec>(), s);
+                           h->deg.as<uint32_t>(), h->cap.as<uint32_t>(), h->vrec.as<ERec>(), h->row_epoch.as<uint32_t>(), s);
         h->pool_used += grow;
         h->m = m_new;
         // records: the source rows' slots (anchors reset), then every slot whose
@@ -876,6 +1110,7 @@ int wharf_destroy_index(wharf_handle* h)
         REQUIRE(h, WHARF_E_INVALID, "null handle");
         h->ensure_walks();
         launch_fill_u32(h->walks.as<uint32_t>(), h->W * h->L, kSent, h->s);
+        h->walks_changed();
         h->sync();
         h->has_walks = false;
     });
@@ -887,6 +1122,8 @@ int wharf_generate(wharf_handle* h)
         REQUIRE(h, WHARF_E_INVALID, "null handle");
         auto t0 = std::chrono::steady_clock::now();
         HIPCHK(hipMemsetAsync(h->counters.p, 0, 16, h->s));
+        HIPCHK(hipMemsetAsync(h->counters.as<unsigned long long>() + 7, 0, 8, h->s));
+        h->st_park_passes = 0;
         WalkArgs a = h->walk_args();
         HIPCHK(hipEventRecord(h->ev[0], h->s));
         // node2vec MH with a cold anchor cache and many more steps than states:
@@ -911,6 +1148,7 @@ int wharf_generate(wharf_handle* h)
             }
         }
         h->anchors_cold = false;
+        h->walks_changed();
         launch_walk(a, false, h->s);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(h->ev[1], h->s));
@@ -942,7 +1180,7 @@ int wharf_batch_walk_update(wharf_handle* h, const uint32_t* sources, uint64_t k
         REQUIRE(k == 0 || sources, WHARF_E_INVALID, "sources is null");
         auto t0 = std::chrono::steady_clock::now();
         h->st.affected = 0;
-        h->st.steps = h->st.accepts = 0;
+        h->st.steps = h->st.accepts = h->st.last_anchor_inits = h->st.last_rewalk_passes = 0;
         h->st.batch_edges = 0;
         h->st.last_graph_update_ms = h->st.last_walk_update_ms = h->st.last_walk_kernel_ms = 0;
         h->st.last_csr_move_ms = 0;
@@ -1000,8 +1238,11 @@ int wharf_set_shard(wharf_handle* h, uint64_t lo, uint64_t hi)
         REQUIRE(lo <= hi && hi <= h->n, WHARF_E_INVALID, "shard range must satisfy lo <= hi <= n");
         h->sync();
         h->walks.release();
+        h->walks_changed();
+        h->free_snaps();
         h->aff.release();
         h->defer.release();
+        h->park.release();
         h->lo = lo;
         h->hi = hi;
         h->n_loc = hi - lo;
@@ -1046,10 +1287,7 @@ int wharf_walk(wharf_handle* h, uint64_t wid, uint32_t* out, uint32_t* len)
         REQUIRE(h && out && len, WHARF_E_INVALID, "null argument");
         const uint64_t li = local_index(h, wid);
         h->ensure_walks();
-        h->sel.ensure(h->L * 4);
-        launch_gather_walk(h->walks.as<uint32_t>(), h->W, h->L, li, h->sel.as<uint32_t>(), h->s);
-        HIPCHK(hipMemcpyAsync(out, h->sel.p, h->L * 4, hipMemcpyDeviceToHost, h->s));
-        h->sync();
+        std::memcpy(out, h->snap_row(li), h->L * 4);
         uint32_t c = 0;
         while (c < h->L && out[c] != kSent) c++;
         *len = c;
@@ -1082,8 +1320,7 @@ int wharf_vertex_at_walk(wharf_handle* h, uint64_t wid, uint32_t position, uint3
         REQUIRE(position < h->L, WHARF_E_RANGE, "position >= walk_length");
         const uint64_t li = local_index(h, wid);
         h->ensure_walks();
-        HIPCHK(hipMemcpyAsync(vertex, h->walks.as<uint32_t>() + (uint64_t)position * h->W + li, 4, hipMemcpyDeviceToHost, h->s));
-        h->sync();
+        *vertex = h->snap_row(li)[position];
     });
 }
 
@@ -1338,7 +1575,7 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->erec2.cap + h->scratch.cap + h->rplan.cap + h->pscan.cap;
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
                       h->runs.cap + h->fplan.cap + h->memo.cap + h->srcidx.cap + h->count.cap + h->pairs.cap +
-                      h->sel.cap + h->defer.cap + h->stab.cap + h->preoff.cap + h->rtab.cap + h->bitmap.cap + h->counters.cap +
+                      h->sel.cap + h->defer.cap + h->park.cap + h->parkc.cap + h->stab.cap + h->preoff.cap + h->rtab.cap + h->bitmap.cap + h->counters.cap +
                       h->errflag.cap;
     r.total_bytes = r.csr_bytes + r.records_bytes + r.walks_bytes + r.samplers_bytes + r.edge_hash_bytes +
                     r.update_buffers_bytes + r.scratch_bytes;
@@ -1359,6 +1596,7 @@ int wharf_get_stats(const wharf_handle* h, wharf_stats* out)
     out->pool_capacity = h->pool_cap;
     out->last_moved_row_slots = h->grown;
     out->repacks = h->repacks;
+    out->dead_slots = h->dead_slots;
     return WHARF_OK;
 }
 

@@ -35,7 +35,7 @@ struct WalkArgs {
     const uint32_t* bitmap;      // batch sources (re-walk)
     const uint32_t* bloom;       // Bloom filter of the batch sources, kBloomWords
     uint8_t* aff;                // per owned walk: re-walk position or kNoRewalk
-    unsigned long long* counters;  // [0] steps, [1] accepts
+    unsigned long long* counters;  // [0] steps, [1] accepts, [2] re-walk list, [3..6] WHARF_INIT_STATS, [7] anchor inits
     uint64_t n, n_loc, lo, W;
     uint32_t L, epoch;
     uint32_t key0, key1;
@@ -54,7 +54,11 @@ struct WalkArgs {
                                  // (the table has kMemoPad readable words on either side)
     uint32_t wpv;
     int nt_rows;                 // chunked scans: non-temporal walk-matrix row loads (most walks re-walk)
+    int park;                    // node2vec MH re-walk by passes (k_rewalk_park / k_park_init), run by the host
 };
+
+constexpr uint64_t kListMask = (1ull << 40) - 1;   // counters[2]: tickets << 40 | re-walk list entries
+constexpr uint64_t kParkRecBytes = 32;   // one parked walker of the node2vec re-walk passes
 
 
 // per batch source: the new row (slack-row CSR update, k_plan_rows .. k_commit_rows)
@@ -69,6 +73,11 @@ unsigned grid_for(uint64_t work, unsigned block);
 unsigned cu_count();
 
 void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s);
+// node2vec MH re-walk passes: fresh = the input is k_rewalk_plan's list, park = walkers that need
+// an uncached anchor are appended to `out` instead of initialising it in the wave
+void launch_rewalk_park(const WalkArgs& a, int fresh, int park, const void* in, const unsigned long long* in_cnt,
+                        void* out, unsigned long long* out_cnt, hipStream_t s);
+void launch_park_init(const WalkArgs& a, const void* in, const unsigned long long* in_cnt, hipStream_t s);
 void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStream_t s);
 void launch_source_degrees(const RunInfo* runs, uint64_t k, const ERec* vrec, uint64_t* out, hipStream_t s);
 void launch_anchor_preinit(const WalkArgs& a, const uint64_t* preoff, uint64_t k, hipStream_t s);
@@ -88,8 +97,7 @@ void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off
                          int insert, uint32_t* chg, hipStream_t s);
 void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_t s);
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
-                     const uint32_t* deg, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, uint32_t* row_epoch,
-                     uint32_t epoch, hipStream_t s);
+                     const uint32_t* deg, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, hipStream_t s);
 void launch_mark_sources(const uint32_t* src, uint64_t k, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom,
                          hipStream_t s);
 void launch_row_degrees(const uint64_t* coff, uint64_t n, uint32_t* deg, uint32_t* cap, uint64_t* capw, int slack,
@@ -99,20 +107,29 @@ void launch_deg_u64(const uint32_t* deg, uint64_t n, uint64_t* out, hipStream_t 
 void launch_copy_rows(const uint64_t* soff, const uint32_t* deg, const uint32_t* src, const uint64_t* doff, uint64_t n,
                       uint32_t* dst, const uint64_t* sanc, uint64_t* danc, hipStream_t s);
 void launch_plan_rows(const RunInfo* runs, uint64_t k, const uint32_t* cap, const uint32_t* cf, int insert, int slack,
-                      uint64_t* need, uint64_t* save, RowPlan* plan, hipStream_t s);
+                      uint64_t* need, uint64_t* save, RowPlan* plan, unsigned long long* dead, hipStream_t s);
+// in-place pool compaction (wharf_handle::compact)
+void launch_slot_order_keys(const uint64_t* off, const uint32_t* cap, uint64_t n, uint64_t* keys, uint32_t* vals,
+                            hipStream_t s);
+void launch_ordered_caps(const uint32_t* order, const uint32_t* cap, uint64_t n, uint64_t* capw, hipStream_t s);
+void launch_compact_gather(const uint32_t* order, const uint64_t* snoff, uint64_t r0, uint64_t r1, const uint64_t* off,
+                           const uint32_t* deg, const uint32_t* adj, const uint64_t* anc, uint64_t D, uint64_t C,
+                           uint32_t* sadj, uint64_t* sanc, hipStream_t s);
+void launch_compact_put(const uint32_t* sadj, const uint64_t* sanc, uint64_t cnt, uint64_t D, uint32_t* adj,
+                        uint64_t* anc, hipStream_t s);
+void launch_scatter_offsets(const uint32_t* order, const uint64_t* snoff, uint64_t n, uint64_t* off, hipStream_t s);
 void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* adj, const uint64_t* sofs, uint32_t* scratch,
                       hipStream_t s);
 void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint64_t* bkeys, const uint32_t* chg, const uint32_t* cf,
                        const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs, uint64_t pool_end,
                        int insert, RowPlan* plan, uint32_t* adj, hipStream_t s);
 void launch_commit_rows(const RunInfo* runs, uint64_t k, const RowPlan* plan, uint32_t epoch, uint64_t* off,
-                        uint32_t* deg, uint32_t* cap, ERec* vrec, hipStream_t s);
+                        uint32_t* deg, uint32_t* cap, ERec* vrec, uint32_t* row_epoch, hipStream_t s);
 void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* off, const uint32_t* deg, const uint32_t* adj,
                       const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s);
 void launch_patch_in_edges(const uint32_t* adj, uint64_t slots, const uint32_t* bitmap, const uint32_t* bloom,
                            const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s);
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s);
-void launch_gather_walk(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* out, hipStream_t s);
 void launch_gather_rows(const uint32_t* walks, uint64_t W, uint32_t L, const uint64_t* list, uint64_t base,
                         uint64_t count, uint32_t* out, hipStream_t s);
 void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint32_t v0, uint32_t v1, uint64_t* len,

@@ -299,13 +299,20 @@ __device__ __forceinline__ void anchor_lookup(const WalkArgs& a, const Row& rc, 
     }
 }
 
-// Called by every active lane of the wave together (WEIGHT inits are wave-cooperative).
-__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, uint64_t* ac,
-                                               uint64_t anc, uint32_t& cls)
+// anchors computed (MH sampler inits): counters[7], one atomic per wave
+__device__ __forceinline__ void count_inits(const WalkArgs& a, bool need)
 {
-    uint32_t an = 0;
-    bool need;
-    anchor_lookup(a, rc, rp, ac, anc, an, cls, need);
+    const uint64_t m = __ballot(need);
+    if (m && __lane_id() == (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(a.counters + 7, (unsigned long long)__popcll(m));
+}
+
+// The anchor of a state whose cache entry is empty (need), computed and
+// cached.  Called by every active lane of the wave together (WEIGHT inits are
+// wave-cooperative); lanes with need = false pass an / cls through.
+__device__ __forceinline__ uint32_t anchor_fill(const WalkArgs& a, bool need, const Row& rc, const Row& rp,
+                                                uint64_t* ac, uint64_t anc, uint32_t an, uint32_t& cls)
+{
+    count_inits(a, need);
     if (a.init == kInitWeight) {
         anchor_init_wave(a, need, rc, rp, an, cls);
     } else if (need) {
@@ -326,6 +333,20 @@ __device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc,
     if (need && ac) *ac = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     return an;
 }
+
+__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, uint64_t* ac,
+                                               uint64_t anc, uint32_t& cls)
+{
+    uint32_t an = 0;
+    bool need;
+    anchor_lookup(a, rc, rp, ac, anc, an, cls, need);
+    return anchor_fill(a, need, rc, rp, ac, anc, an, cls);
+}
+
+// Heaviest weight class (node2vec.h:74-88: 1/p, 1, 1/q) and the lightest a
+// non-return candidate can have (triangle 1 or outward 1/q).
+__device__ __forceinline__ float w_heaviest(const WalkArgs& a) { return fmaxf(fmaxf(a.inv_p, 1.0f), a.inv_q); }
+__device__ __forceinline__ float w_lightest_nonreturn(const WalkArgs& a) { return fminf(1.0f, a.inv_q); }
 
 // ---------------------------------------------------------------------------
 // The walk kernels.  One lane per walk; lane li owns walk matrix column li.
@@ -357,9 +378,14 @@ __device__ __forceinline__ Row load_edge(const WalkArgs& a, uint64_t e, uint64_t
 // node2vec.h:52-72 through MetropolisHastingsSampler::sample, or the
 // deterministic adj(cur)[Random(wid/n).lrand() % deg] of wharfmh.h:296-304).
 // Advances the walker; returns the new vertex.
-template <int MODEL, bool DET>
+// PARK (node2vec MH re-walk by passes, k_rewalk_park): a state whose anchor is
+// not cached and is needed for the decision is not initialised here; the step
+// returns with `parked` set and the walker unchanged, and k_park_init computes
+// the anchor with full waves before the walker resumes.
+template <int MODEL, bool DET, bool PARK = false>
 __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, const uint64_t* __restrict__ rt,
-                                              uint32_t pos, uint32_t wlo, uint32_t whi, uint32_t ep, uint32_t& accepts)
+                                              uint32_t pos, uint32_t wlo, uint32_t whi, uint32_t ep, uint32_t& accepts,
+                                              bool* parked = nullptr)
 {
     Row nx;
     if constexpr (DET) {
@@ -374,23 +400,41 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
             accepts++;   // weights are all 1: sample() always accepts
             nx = cand;
         } else {
-            uint32_t acls;
-            const uint32_t ai = anchor_get(a, w.rc, w.rp, w.ac, w.anc, acls);
+            // metropolis_hastings_sampler.h:118-122: accept iff w(a) < w(c) or
+            // u <= w(c) / w(a).  A non-return candidate weighs 1 (triangle) or
+            // 1/q (outward); when both weights give the same decision the
+            // class, and so the has_edge probe, cannot matter (on sparse-
+            // triangle graphs the anchor is mostly outward, and an outward
+            // anchor accepts every candidate).
+            const double u = u01(q.x1, q.x2);
+            auto accept = [&](float wc, float wa) { return (wa < wc) || (u <= (double)wc / (double)wa); };
+            uint32_t acls = 0, ai = 0;
+            bool need;
+            anchor_lookup(a, w.rc, w.rp, w.ac, w.anc, ai, acls, need);
+            // The decision falls monotonically with w(a) and rises with w(c): a
+            // candidate accepted against the heaviest class with its lightest
+            // possible weight is accepted whatever the anchor is, so an anchor
+            // that is not cached yet is not computed for it (exact; the entry
+            // stays empty for a later walker that needs it).  In the sparse
+            // re-walks of configs[4] 79 % of the steps enter a state with no
+            // cached anchor; p = .5, q = 2 settles a quarter of them here.
+            const bool sure = need && accept(cand.v == w.rp.v ? a.inv_p : w_lightest_nonreturn(a), w_heaviest(a));
+            const bool init = need && !sure;
+            if constexpr (PARK) {
+                if (init) {
+                    *parked = true;
+                    return 0;
+                }
+            } else {
+                ai = anchor_fill(a, init, w.rc, w.rp, w.ac, w.anc, ai, acls);
+            }
             bool ok = true;   // proposing the anchor itself is always accepted
-            if (ai != ci) {
-                // metropolis_hastings_sampler.h:118-122: accept iff w(a) < w(c) or
-                // u <= w(c) / w(a).  A non-return candidate weighs 1 (triangle) or
-                // 1/q (outward); when both weights give the same decision the
-                // class, and so the has_edge probe, cannot matter (on sparse-
-                // triangle graphs the anchor is mostly outward, and an outward
-                // anchor accepts every candidate).
+            if (!sure && ai != ci) {
                 const float wa = class_weight(a, acls);
-                const double u = u01(q.x1, q.x2);
-                auto accept = [&](float wc) { return (wa < wc) || (u <= (double)wc / (double)wa); };
                 if (cand.v == w.rp.v) {
-                    ok = accept(a.inv_p);
+                    ok = accept(a.inv_p, wa);
                 } else {
-                    const bool ok_tri = accept(1.0f), ok_out = accept(a.inv_q);
+                    const bool ok_tri = accept(1.0f, wa), ok_out = accept(a.inv_q, wa);
                     ok = ok_tri == ok_out ? ok_tri : (has_edge(a, w.rp, cand.v) ? ok_tri : ok_out);
                 }
             }
@@ -502,6 +546,7 @@ __device__ __forceinline__ void walk_state(const WalkArgs& a, uint32_t cur, uint
 __device__ __forceinline__ void anchor_compute(const WalkArgs& a, bool need, const Row& rc, const Row& rp,
                                                uint32_t& an, uint32_t& cls)
 {
+    count_inits(a, need);
     if (a.init == kInitWeight) anchor_init_wave<WHARF_PREINIT_ROUNDS>(a, need, rc, rp, an, cls);
     else if (need) an = anchor_init(a, rc, rp, cls);
 }
@@ -1047,7 +1092,6 @@ void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStr
 // list kernel): configs[2] node2vec batch 73.7 -> 63.6 ms, configs[4]-shaped
 // (scale 24, wpv 1) re-walk 51.7 / 43.9 -> 39.1 / 31.5 ms; the flattened
 // kernel over the same sorted list: 104 ms / 47.9 ms (scattered stores).
-constexpr uint64_t kListMask = (1ull << 40) - 1;   // counters[2]: tickets << 40 | list entries
 
 // The rewalk point of lane li's walk by the chunked scan of k_rewalk_chunked<false>
 // (kScanChunk rows per round trip, the next chunk's rows in flight while this
@@ -1251,6 +1295,137 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
     wave_add(a.counters + 1, accepts);
 }
 
+// node2vec MH re-walk by passes (sparse walks: configs[4]'s 1/8 shard, where
+// 79 % of the re-walk steps enter a state whose anchor was never computed).
+// In the lock-step kernels above each such init stalls its wave for rounds of
+// dependent proposal loads while few lanes have one.  Here a walker that needs
+// an anchor PARKS instead: k_rewalk_park advances every walker of its input
+// list (lanes at their own pace, a lane whose walker parks or ends takes the
+// next entry) and appends the parked ones {walk | pos, cur, prev, cache entry}
+// to an output list (one atomic per wave, ballot + prefix rank); k_park_init
+// then computes the anchors of the whole list with every lane of every wave
+// initialising (anchor_init_wave over full waves, as k_anchor_init_all), and
+// the next pass resumes the walkers.  Anchors are a pure function of the
+// snapshot, so the corpus, step and acceptance counts equal the lock-step
+// kernels' (the parity suite forces this path).  The host runs passes until the
+// list is short, then finishes it with lazy inits (PARK = false).
+struct ParkRec {
+    uint64_t lp;         // walk column | next position << 56
+    uint32_t cur, prev;  // the walker's state
+    uint64_t* ac;        // its anchor cache entry (edge record or start-state table), or null:
+    uint64_t own;        //   a state without one (a re-walk start whose edge prev -> cur is gone)
+                         //   gets its anchor here, for the walker that resumes from this record
+};
+
+template <int MODEL, bool FRESH, bool PARK>
+__global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* in,
+                                                     const unsigned long long* __restrict__ in_cnt,
+                                                     ParkRec* __restrict__ out, unsigned long long* __restrict__ out_cnt)
+{
+    uint32_t steps = 0, accepts = 0;
+    const uint64_t cnt = FRESH ? (a.counters[2] & kListMask) : *in_cnt;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t* __restrict__ walks = a.walks;
+    const uint64_t W = a.W;
+    const uint32_t L = a.L, ep = a.epoch << 4;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t li = 0;
+    uint32_t pos = L, wlo = 0, whi = 0;
+    Walker w;
+    w.rc.deg = 0;
+    bool has = false;
+    for (;;) {
+        if (!has && i < cnt) {   // this lane's next walker
+            if constexpr (FRESH) {
+                const uint64_t e = a.defer[i];
+                li = e & ((1ull << 56) - 1);
+                const uint32_t p = (uint32_t)(e >> 56);
+                pos = p + 1;
+                const uint64_t r = li / a.n_loc;
+                const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
+                wlo = (uint32_t)wid;
+                whi = (uint32_t)(wid >> 32);
+                const uint32_t x = walks[(uint64_t)p * W + li];
+                const uint32_t xprev = p ? walks[(uint64_t)(p - 1) * W + li] : x;
+                walk_state<MODEL, false>(a, x, xprev, p, wlo, whi, ep, w);
+            } else {
+                const ParkRec pr = in[i];
+                li = pr.lp & ((1ull << 56) - 1);
+                pos = (uint32_t)(pr.lp >> 56);
+                const uint64_t r = li / a.n_loc;
+                const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
+                wlo = (uint32_t)wid;
+                whi = (uint32_t)(wid >> 32);
+                w.rc = load_rec(a.vrec, pr.cur);
+                w.rp = load_rec(a.vrec, pr.prev);
+                w.ac = pr.ac ? pr.ac : const_cast<uint64_t*>(&in[i].own);   // (k_park_init filled it)
+                w.anc = *w.ac;
+            }
+            has = pos < L;
+            i += stride;
+        }
+        if (!__any(has)) break;
+        bool park = false;
+        if (has) {
+            uint32_t val = kSent;
+            const bool live = w.rc.deg != 0;   // a walk at a vertex without out-edges ends
+            if (live) val = walk_step<MODEL, false, PARK>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, &park);
+            if (!park) {
+                steps += live;
+                walks[(uint64_t)pos * W + li] = val;
+                has = ++pos < L;
+            }
+        }
+        if constexpr (PARK) {
+            const uint64_t pm = __ballot(park);
+            if (pm) {
+                unsigned long long base = 0;
+                if (__lane_id() == 0) base = atomicAdd(out_cnt, (unsigned long long)__popcll(pm));
+                base = __shfl(base, 0, 64);
+                if (park) {
+                    out[base + __popcll(pm & ((1ull << __lane_id()) - 1))] =
+                        ParkRec{li | ((uint64_t)pos << 56), w.rc.v, w.rp.v, w.ac, kAnchorNone64};
+                    has = false;
+                }
+            }
+        }
+    }
+    wave_add(a.counters + 0, steps);
+    wave_add(a.counters + 1, accepts);
+}
+
+// The anchors of the parked states, one per lane over full waves.
+__global__ __launch_bounds__(256) void k_park_init(WalkArgs a, ParkRec* in, const unsigned long long* __restrict__ in_cnt)
+{
+    const uint64_t cnt = *in_cnt;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < cnt; t += stride) {
+        const ParkRec pr = in[t];
+        const Row rc = load_rec(a.vrec, pr.cur), rp = load_rec(a.vrec, pr.prev);
+        uint32_t an = 0, cls = 0;
+        anchor_compute(a, true, rc, rp, an, cls);
+        *(pr.ac ? pr.ac : &in[t].own) = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+    }
+}
+
+void launch_rewalk_park(const WalkArgs& a, int fresh, int park, const void* in, const unsigned long long* in_cnt,
+                        void* out, unsigned long long* out_cnt, hipStream_t s)
+{
+    const dim3 grid(cu_count() * 8), block(256);   // resident lanes (8 blocks of 256 per CU)
+    const ParkRec* pin = reinterpret_cast<const ParkRec*>(in);
+    ParkRec* pout = reinterpret_cast<ParkRec*>(out);
+    if (fresh && park) hipLaunchKernelGGL((k_rewalk_park<kNode2Vec, true, true>), grid, block, 0, s, a, pin, in_cnt, pout, out_cnt);
+    else if (fresh) hipLaunchKernelGGL((k_rewalk_park<kNode2Vec, true, false>), grid, block, 0, s, a, pin, in_cnt, pout, out_cnt);
+    else if (park) hipLaunchKernelGGL((k_rewalk_park<kNode2Vec, false, true>), grid, block, 0, s, a, pin, in_cnt, pout, out_cnt);
+    else hipLaunchKernelGGL((k_rewalk_park<kNode2Vec, false, false>), grid, block, 0, s, a, pin, in_cnt, pout, out_cnt);
+}
+
+void launch_park_init(const WalkArgs& a, const void* in, const unsigned long long* in_cnt, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_park_init, cu_count() * 8, 256, 0, s, a, reinterpret_cast<ParkRec*>(const_cast<void*>(in)),
+                       in_cnt);
+}
+
 // Blocks for the walk kernels: one walk per lane by default; a smaller grid of
 // lanes each looping over several walks with WHARF_WALK_BLOCKS_PER_CU=k
 // (k blocks of 256 per CU; 0 = one walk per lane).
@@ -1299,7 +1474,7 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
     do {                                                                                     \
         if (rewalk && M == kNode2Vec) {                                                      \
             hipLaunchKernelGGL(k_rewalk_plan, grid, block, 0, s, a);                         \
-            if (!a.scan_only) {                                                              \
+            if (!a.scan_only && !a.park) { /* park: the host runs the passes */              \
                 if (flat_list()) hipLaunchKernelGGL((k_rewalk_list<M, D>), lgrid, block, 0, s, a); \
                 else hipLaunchKernelGGL((k_rewalk_sorted<M, D>), lgrid, block, 0, s, a);     \
             }                                                                                \
@@ -1617,9 +1792,7 @@ __global__ void k_run_flags(const uint64_t* __restrict__ bkeys, uint64_t mb, uin
 // per source run j: src, old row [off, end), batch run [rs, re)
 __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ run_start, uint64_t k,
                            uint64_t mb, const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg,
-                           RunInfo* __restrict__ runs,
-                           uint32_t* __restrict__ bitmap, uint32_t* __restrict__ bloom, uint32_t* __restrict__ row_epoch,
-                           uint32_t epoch)
+                           RunInfo* __restrict__ runs, uint32_t* __restrict__ bitmap, uint32_t* __restrict__ bloom)
 {
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t rs = run_start[j];
@@ -1632,7 +1805,6 @@ __global__ void k_run_info(const uint64_t* __restrict__ bkeys, const uint32_t* _
         const uint32_t h = bloom_mix(s);
         atomicOr(bloom + bloom_word(h), bloom_bits(h));
         atomicOr(bloom + kBloomWords + bloom_word_big(h), bloom_bits(h));
-        if (row_epoch) row_epoch[s] = epoch;   // the source's samplers are reset (wharfmh.h:504,539)
     }
 }
 
@@ -1725,7 +1897,7 @@ __global__ void k_copy_rows(const uint64_t* __restrict__ soff, const uint32_t* _
 // scratch copy the merge reads)
 __global__ void k_plan_rows(const RunInfo* __restrict__ runs, uint64_t k, const uint32_t* __restrict__ cap,
                             const uint32_t* __restrict__ cf, int insert, int slack, uint64_t* __restrict__ need,
-                            uint64_t* __restrict__ save, RowPlan* __restrict__ plan)
+                            uint64_t* __restrict__ save, RowPlan* __restrict__ plan, unsigned long long* __restrict__ dead)
 {
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= k; j += (uint64_t)gridDim.x * blockDim.x) {
         if (j == k) { need[k] = 0; save[k] = 0; continue; }
@@ -1738,6 +1910,7 @@ __global__ void k_plan_rows(const RunInfo* __restrict__ runs, uint64_t k, const 
         need[j] = reloc ? nc : 0;
         save[j] = d;
         plan[j] = RowPlan{reloc ? kRelocate : ri.off, nd, nc, c};
+        if (reloc && c) atomicAdd(dead, (unsigned long long)c);   // the row's old place becomes kGap
     }
 }
 
@@ -1818,10 +1991,12 @@ __global__ void k_merge_rows(const RunInfo* __restrict__ runs, const uint64_t* _
     if (threadIdx.x == 0) plan[j].noff = noff;
 }
 
-// per run: the source's new row and record (its epoch was set by k_run_info)
+// per run: the source's new row and record, and its row epoch: the source's
+// samplers are reset (wharfmh.h:504,539).  Runs after the last point where the
+// batch can fail (the pool planning), so a failed batch leaves no epoch behind.
 __global__ void k_commit_rows(const RunInfo* __restrict__ runs, uint64_t k, const RowPlan* __restrict__ plan,
                               uint32_t epoch, uint64_t* __restrict__ off, uint32_t* __restrict__ deg,
-                              uint32_t* __restrict__ cap, ERec* __restrict__ vrec)
+                              uint32_t* __restrict__ cap, ERec* __restrict__ vrec, uint32_t* __restrict__ row_epoch)
 {
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t s = runs[j].src;
@@ -1830,6 +2005,7 @@ __global__ void k_commit_rows(const RunInfo* __restrict__ runs, uint64_t k, cons
         deg[s] = p.ndeg;
         cap[s] = p.ncap;
         vrec[s] = make_rec(s, p.ndeg, p.noff, epoch);
+        if (row_epoch) row_epoch[s] = epoch;
     }
 }
 
@@ -1927,11 +2103,6 @@ __global__ void k_transpose(const uint32_t* __restrict__ in, uint64_t W, uint32_
         const uint32_t p = p0 + tx;
         if (p < L && w < W) out[w * L + p] = tile[tx][r];
     }
-}
-
-__global__ void k_gather_walk(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* __restrict__ out)
-{
-    for (uint32_t p = threadIdx.x; p < L; p += blockDim.x) out[p] = walks[(uint64_t)p * W + li];
 }
 
 // rows out[i][p] = walks[p][li(i)], li(i) = list ? list[i] : base + i
@@ -2154,9 +2325,8 @@ void launch_batch_change(const uint64_t* bkeys, uint64_t mb, const uint64_t* off
 void launch_run_flags(const uint64_t* bkeys, uint64_t mb, uint8_t* f, hipStream_t s)
 { hipLaunchKernelGGL(k_run_flags, grid_for(mb, 256), 256, 0, s, bkeys, mb, f); }
 void launch_run_info(const uint64_t* bkeys, const uint32_t* run_start, uint64_t k, uint64_t mb, const uint64_t* off,
-                     const uint32_t* deg, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, uint32_t* row_epoch,
-                     uint32_t epoch, hipStream_t s)
-{ hipLaunchKernelGGL(k_run_info, grid_for(k, 256), 256, 0, s, bkeys, run_start, k, mb, off, deg, runs, bitmap, bloom, row_epoch, epoch); }
+                     const uint32_t* deg, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, hipStream_t s)
+{ hipLaunchKernelGGL(k_run_info, grid_for(k, 256), 256, 0, s, bkeys, run_start, k, mb, off, deg, runs, bitmap, bloom); }
 
 void launch_mark_sources(const uint32_t* src, uint64_t k, RunInfo* runs, uint32_t* bitmap, uint32_t* bloom, hipStream_t s)
 {
@@ -2173,8 +2343,84 @@ void launch_copy_rows(const uint64_t* soff, const uint32_t* deg, const uint32_t*
                       uint32_t* dst, const uint64_t* sanc, uint64_t* danc, hipStream_t s)
 { if (n) hipLaunchKernelGGL(k_copy_rows, (unsigned)((n + 63) / 64), 256, 0, s, soff, deg, src, doff, n, dst, sanc, danc); }
 void launch_plan_rows(const RunInfo* runs, uint64_t k, const uint32_t* cap, const uint32_t* cf, int insert, int slack,
-                      uint64_t* need, uint64_t* save, RowPlan* plan, hipStream_t s)
-{ hipLaunchKernelGGL(k_plan_rows, grid_for(k + 1, 256), 256, 0, s, runs, k, cap, cf, insert, slack, need, save, plan); }
+                      uint64_t* need, uint64_t* save, RowPlan* plan, unsigned long long* dead, hipStream_t s)
+{ hipLaunchKernelGGL(k_plan_rows, grid_for(k + 1, 256), 256, 0, s, runs, k, cap, cf, insert, slack, need, save, plan, dead); }
+
+// In-place pool compaction (the repack that needs no second pool): rows keep
+// their capacities and are packed in slot order, so every row's new start is at
+// or below its old one and the dead slots of moved rows disappear.  The pool is
+// rewritten window by window in ascending order: the slots bound for window
+// [D, D + C) all come from at or above D, which no earlier window has written,
+// so they are first gathered into a staging buffer, then written.
+// order[i] = the row with the i-th smallest start; noff its new start.
+__global__ void k_slot_order_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ cap, uint64_t n,
+                                  uint64_t* __restrict__ keys, uint32_t* __restrict__ vals)
+{
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        keys[v] = off[v];
+        vals[v] = (uint32_t)v;
+    }
+}
+
+__global__ void k_ordered_caps(const uint32_t* __restrict__ order, const uint32_t* __restrict__ cap, uint64_t n,
+                               uint64_t* __restrict__ capw)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (uint64_t)gridDim.x * blockDim.x)
+        capw[i] = i < n ? cap[order[i]] : 0;
+}
+
+// one wave per row of the window's row range [r0, r1) (rows in slot order)
+__global__ void k_compact_gather(const uint32_t* __restrict__ order, const uint64_t* __restrict__ snoff, uint64_t r0,
+                                 uint64_t r1, const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg,
+                                 const uint32_t* __restrict__ adj, const uint64_t* __restrict__ anc, uint64_t D,
+                                 uint64_t C, uint32_t* __restrict__ sadj, uint64_t* __restrict__ sanc)
+{
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t i = r0 + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); i < r1; i += waves) {
+        const uint32_t v = order[i];
+        const uint64_t no = snoff[i], o = off[v], d = deg[v];
+        const uint64_t j0 = D > no ? D - no : 0, j1 = min(d, D + C > no ? D + C - no : 0);
+        for (uint64_t j = j0 + (threadIdx.x & 63); j < j1; j += 64) {
+            sadj[no + j - D] = adj[o + j];
+            if (anc) sanc[no + j - D] = anc[(o + j) * kAnchorStride];
+        }
+    }
+}
+
+__global__ void k_compact_put(const uint32_t* __restrict__ sadj, const uint64_t* __restrict__ sanc, uint64_t cnt,
+                              uint64_t D, uint32_t* __restrict__ adj, uint64_t* __restrict__ anc)
+{
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < cnt; t += (uint64_t)gridDim.x * blockDim.x) {
+        adj[D + t] = sadj[t];
+        if (anc) anc[(D + t) * kAnchorStride] = sanc[t];
+    }
+}
+
+__global__ void k_scatter_offsets(const uint32_t* __restrict__ order, const uint64_t* __restrict__ snoff, uint64_t n,
+                                  uint64_t* __restrict__ off)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (uint64_t)gridDim.x * blockDim.x)
+        off[i < n ? order[i] : n] = snoff[i];
+}
+
+void launch_slot_order_keys(const uint64_t* off, const uint32_t* cap, uint64_t n, uint64_t* keys, uint32_t* vals,
+                            hipStream_t s)
+{ if (n) hipLaunchKernelGGL(k_slot_order_keys, grid_for(n, 256), 256, 0, s, off, cap, n, keys, vals); }
+void launch_ordered_caps(const uint32_t* order, const uint32_t* cap, uint64_t n, uint64_t* capw, hipStream_t s)
+{ hipLaunchKernelGGL(k_ordered_caps, grid_for(n + 1, 256), 256, 0, s, order, cap, n, capw); }
+void launch_compact_gather(const uint32_t* order, const uint64_t* snoff, uint64_t r0, uint64_t r1, const uint64_t* off,
+                           const uint32_t* deg, const uint32_t* adj, const uint64_t* anc, uint64_t D, uint64_t C,
+                           uint32_t* sadj, uint64_t* sanc, hipStream_t s)
+{
+    if (r1 > r0)
+        hipLaunchKernelGGL(k_compact_gather, grid_for((r1 - r0) * 64, 256), 256, 0, s, order, snoff, r0, r1, off, deg,
+                           adj, anc, D, C, sadj, sanc);
+}
+void launch_compact_put(const uint32_t* sadj, const uint64_t* sanc, uint64_t cnt, uint64_t D, uint32_t* adj,
+                        uint64_t* anc, hipStream_t s)
+{ if (cnt) hipLaunchKernelGGL(k_compact_put, grid_for(cnt, 256), 256, 0, s, sadj, sanc, cnt, D, adj, anc); }
+void launch_scatter_offsets(const uint32_t* order, const uint64_t* snoff, uint64_t n, uint64_t* off, hipStream_t s)
+{ hipLaunchKernelGGL(k_scatter_offsets, grid_for(n + 1, 256), 256, 0, s, order, snoff, n, off); }
 void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* adj, const uint64_t* sofs, uint32_t* scratch,
                       hipStream_t s)
 { if (k) hipLaunchKernelGGL(k_save_rows, (unsigned)k, 256, 0, s, runs, adj, sofs, scratch); }
@@ -2186,8 +2432,8 @@ void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint64_t* bkeys, c
                               pool_end, insert, plan, adj);
 }
 void launch_commit_rows(const RunInfo* runs, uint64_t k, const RowPlan* plan, uint32_t epoch, uint64_t* off,
-                        uint32_t* deg, uint32_t* cap, ERec* vrec, hipStream_t s)
-{ if (k) hipLaunchKernelGGL(k_commit_rows, grid_for(k, 256), 256, 0, s, runs, k, plan, epoch, off, deg, cap, vrec); }
+                        uint32_t* deg, uint32_t* cap, ERec* vrec, uint32_t* row_epoch, hipStream_t s)
+{ if (k) hipLaunchKernelGGL(k_commit_rows, grid_for(k, 256), 256, 0, s, runs, k, plan, epoch, off, deg, cap, vrec, row_epoch); }
 void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* off, const uint32_t* deg, const uint32_t* adj,
                       const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s)
 { if (k) hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, off, deg, adj, vrec, erec, rs); }
@@ -2204,8 +2450,6 @@ void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out,
     const dim3 g((unsigned)((W + 63) / 64), (L + 63) / 64);
     hipLaunchKernelGGL(k_transpose, g, 256, 0, s, in, W, L, out);
 }
-void launch_gather_walk(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t li, uint32_t* out, hipStream_t s)
-{ hipLaunchKernelGGL(k_gather_walk, 1, 256, 0, s, walks, W, L, li, out); }
 void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint32_t v0, uint32_t v1, uint64_t* len,
                          hipStream_t s)
 { hipLaunchKernelGGL(k_walk_lengths, grid_for(W, 256), 256, 0, s, walks, W, L, v0, v1, len); }

@@ -29,12 +29,21 @@
 
 #include <sys/time.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <functional>
 #include <iomanip>
 #include <iostream>
 #include <limits>
+#include <map>
+#include <memory>
+#include <set>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <tuple>
@@ -47,12 +56,12 @@
 using uintV = uint32_t;
 using uintE = uint64_t;
 
-// names the reference's headers make visible unqualified
-using std::cout;
-using std::endl;
-using std::get;
-using std::string;
-using std::tuple;
+// The reference's <wharfmh.h> makes namespace std visible to its drivers
+// (libs/compressed_trees/common/IO.h:22 and trees/map.h:3 say `using namespace
+// std;`, reached through graph/api.h), and they rely on it: `string`,
+// `stringstream`, `ofstream` unqualified (experiments/src/vertex-classification.cpp:
+// 8,124,142), with the standard headers above that the reference's headers pull in.
+using namespace std;
 
 namespace types {
 using Vertex = uintV;

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define WHARF_ABI_VERSION 3
+#define WHARF_ABI_VERSION 4
 
 enum {
     WHARF_OK = 0,
@@ -80,12 +80,17 @@ typedef struct wharf_stats {
     uint64_t hbm_bytes_graph;      /* resident bytes: CSR + vertex records (+ anchors) */
     double   last_csr_move_ms;     /* device time of the last update's streaming pass over the slot pool
                                       (k_patch_in_edges: the in-edge records of the batch sources) */
-    uint64_t last_moved_slots;     /* pool slots that pass read */
+    uint64_t last_moved_slots;     /* pool slots that pass read (scanned: live, slack and dead slots alike) */
     /* slack-row CSR: row v = slots [off, off + deg) of a pool with cap >= deg reserved */
     uint64_t pool_slots;           /* slots handed out to rows (live edges + slack + rows' old places) */
     uint64_t pool_capacity;        /* slots allocated */
     uint64_t last_moved_row_slots; /* slots given to rows that outgrew their place in the last batch */
-    uint64_t repacks;              /* pool repacks (fresh slack for every row) so far */
+    uint64_t repacks;              /* pool repacks (fresh slack for every row, or dead slots squeezed out) so far */
+    uint64_t dead_slots;           /* slots of rows' old places (moved rows leave them kGap): read by every
+                                      in-edge pass until a repack reclaims them (one is started past 1/4 of the pool) */
+    uint64_t last_anchor_inits;    /* node2vec MH: anchors (MH sampler inits) computed by the last generate/update */
+    uint64_t last_rewalk_passes;   /* node2vec MH re-walk by passes (k_rewalk_park): passes of the last update,
+                                      0 when the lock-step kernel ran */
 } wharf_stats;
 
 typedef struct wharf_handle wharf_handle;

@@ -8,7 +8,8 @@ the GPU box); the committed outputs are data: inputs and the reference's
 outputs for them.
 
     python tests/golden/make_golden.py            # writes tests/golden/*
-    python tests/golden/make_golden.py mh-matrix  # only the MH statistics matrix (merged into golden.json)
+    python tests/golden/make_golden.py mh-matrix  # only the MH statistics matrices (merged into golden.json)
+    python tests/golden/make_golden.py mh-stream  # only the MH stream cells
 """
 from __future__ import annotations
 
@@ -153,65 +154,112 @@ def mh_matrix(tmp, woff, wadj):
     return out
 
 
-MH_STREAM_BATCHES = ((5000, 0), (3000, 100))   # (edges, seed offset): insert, then delete
+# MH stream cells (wharfmh.h:439-923 in MH mode: re-walks draw from config::random,
+# sampler resets of batch sources at :504,539,652,689).  Per cell: graph, batch
+# pattern, (p, q), sampler init.
+#   undirected: insert 5000 undirected RMAT samples (batch seed s), then delete
+#     3000 (batch seed s + 100), on wiki;
+#   directed: the reference driver's own pattern (throughput-latency.cpp:121,126,135):
+#     insert a directed batch, then delete the same batch, on wiki without its 42
+#     isolated vertices (wiki_compact: a directed edge into an isolated vertex makes
+#     a sink, where the reference evaluates lrand() % 0, utility.h:220, and dies of
+#     SIGFPE).  Batch seeds whose delete would leave a vertex without out-edges are
+#     skipped for the same reason (stream_batch_seeds).
+MH_STREAM_UNDIRECTED = ((True, 5000, 0), (False, 3000, 100))   # (insert?, edges, batch-seed offset)
+MH_STREAM_DIRECTED_EDGES = 5000
+
+
+def stream_cell_specs():
+    """(key, graph, directed, p, q, init) of every stream cell."""
+    out = []
+    for (p, q) in MH_PQ:
+        for init in MH_INITS:
+            out.append((f"undirected_p{p}_q{q}_{init}", "wiki", False, p, q, init))
+    for (p, q) in MH_PQ:
+        for init in MH_INITS:
+            out.append((f"directed_p{p}_q{q}_{init}", "wiki_compact", True, p, q, init))
+    return out
 
 
 def _mh_stream_cell(args):
-    """Reference MH run through an insert and a delete batch (wharfmh.h:439-923
-    in MH mode: re-walks draw from config::random): the final corpus and graph."""
-    tmp, csr, p, q, init, seed = args
-    d = os.path.join(tmp, f"mhs_{p}_{q}_{init}_{seed}")
+    """One reference MH run through the cell's two batches: the class fractions
+    of the final corpus on the final graph."""
+    tmp, csr, key, batches, p, q, init, seed = args
+    d = os.path.join(tmp, f"mhs_{key}_{seed}")
     os.makedirs(d, exist_ok=True)
-    (mi, oi), (md, od) = MH_STREAM_BATCHES
-    run(["out", d, "cfg", 10, 80, "node2vec", p, q, init, 0, seed, "graph-csr", csr, "gen",
-         "ins", mi, seed + oi, 0, "del", md, seed + od, 0, "dump-graph"])
-    wm = read_walks(d, "2_del", 80)
-    off, adj = read_graph(d, "2")
+    cmd = ["out", d, "cfg", 10, 80, "node2vec", p, q, init, 0, seed, "graph-csr", csr, "gen"]
+    for b in batches:
+        cmd += ["ins" if b["insert"] else "del", b["edges"], b["seed"], int(b["directed"])]
+    cmd += ["dump-graph"]
+    run(cmd)
+    wm = read_walks(d, f"{len(batches)}_{'ins' if batches[-1]['insert'] else 'del'}", 80)
+    off, adj = read_graph(d, str(len(batches)))
     shutil.rmtree(d, ignore_errors=True)
     return mh_class_fractions(wm, off, adj)
 
 
 def mh_stream_matrix(tmp, woff, wadj):
-    """MH statistics of the corpus after an insert + delete batch on wiki
-    (undirected RMAT batches generate_batch_of_edges(M, n, seed + offset)),
-    classified against the final graph: pins the re-walk path and the sampler
-    resets of batch sources (wharfmh.h:504,539,652,689) statistically."""
+    """Reference MH statistics of the corpus after an insert and a delete batch,
+    classified against the final graph, per stream cell (stream_cell_specs), 8
+    seeds each: pins the re-walk path and the sampler resets of batch sources
+    statistically, for undirected batches and for the directed insert/delete
+    pairs of the reference's own driver."""
     from concurrent.futures import ThreadPoolExecutor
-    csr = os.path.join(tmp, "wiki_mhs.csr")
-    write_csr(csr, woff, wadj)
-    jobs = [(tmp, csr, 0.5, 2.0, init, s) for init in MH_INITS for s in MH_SEEDS]
+    sys.path.insert(0, os.path.dirname(HERE))   # tests/ (mh_stats)
+    sys.path.insert(0, REPO)                    # oracle/ (generate_batch_of_edges, bit-exact with the reference's)
+    import mh_stats
+    graphs = {"wiki": (woff, wadj), "wiki_compact": mh_stats.wiki_compact(woff, wadj)}
+    paths = {}
+    for gname, (o, a) in graphs.items():
+        paths[gname] = os.path.join(tmp, f"{gname}_mhs.csr")
+        write_csr(paths[gname], o, a)
+    dseeds = mh_stats.stream_batch_seeds(*graphs["wiki_compact"], len(MH_SEEDS), MH_STREAM_DIRECTED_EDGES)
+    jobs, cells = [], {}
+    for key, gname, directed, p, q, init in stream_cell_specs():
+        per_seed = []
+        for i, s in enumerate(MH_SEEDS):
+            if directed:
+                b = dseeds[i]
+                batches = [{"insert": True, "edges": MH_STREAM_DIRECTED_EDGES, "seed": b, "directed": True},
+                           {"insert": False, "edges": MH_STREAM_DIRECTED_EDGES, "seed": b, "directed": True}]
+            else:
+                batches = [{"insert": ins, "edges": e, "seed": s + off, "directed": False}
+                           for (ins, e, off) in MH_STREAM_UNDIRECTED]
+            per_seed.append(batches)
+            jobs.append((tmp, paths[gname], key, batches, p, q, init, s))
+        cells[key] = {"graph": gname, "directed": directed, "p": p, "q": q, "init": init, "batches": per_seed}
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
         res = list(ex.map(_mh_stream_cell, jobs))
-    out = {"seeds": list(MH_SEEDS), "graph": "wiki (tests/golden/wiki_csr.npz)", "wpv": 10, "L": 80,
-           "batches": [{"insert": True, "edges": MH_STREAM_BATCHES[0][0], "seed_offset": MH_STREAM_BATCHES[0][1]},
-                       {"insert": False, "edges": MH_STREAM_BATCHES[1][0], "seed_offset": MH_STREAM_BATCHES[1][1]}],
-           "generator": "ref_harness cfg 10 80 node2vec 0.5 2 <init> 0 <seed> graph-csr wiki gen "
-                        "ins 5000 <seed> 0 del 3000 <seed+100> 0, NUM_THREADS=1 (remove_dups=true)"}
-    cells = {}
+    fr_by = {}
     for j, fr in zip(jobs, res):
-        cells.setdefault(f"node2vec_p{j[2]}_q{j[3]}_{j[4]}", []).append(fr)
-    for key, fr in cells.items():
-        c = {"transitions": [f["transitions"] for f in fr]}
+        fr_by.setdefault(j[2], []).append(fr)
+    for key, fr in fr_by.items():
+        c = cells[key]
+        c["transitions"] = [f["transitions"] for f in fr]
         for k in ("return", "triangle", "outward"):
             v = np.array([f[k] for f in fr])
             c[k] = {"mean": float(v.mean()), "sd": float(v.std(ddof=1)), "per_seed": [float(x) for x in v]}
-        out[key] = c
-    return out
+    return {"seeds": list(MH_SEEDS), "wpv": 10, "L": 80, "cells": cells,
+            "graphs": {"wiki": "tests/golden/wiki_csr.npz",
+                       "wiki_compact": "wiki_csr.npz without its isolated vertices (tests/mh_stats.py wiki_compact)"},
+            "generator": "ref_harness cfg 10 80 node2vec <p> <q> <init> 0 <seed> graph-csr <graph> gen "
+                         "<ins|del> <edges> <batch seed> <directed> x2 dump-graph, NUM_THREADS=1 (remove_dups=true)"}
 
 
-def main_mh_matrix():
+def main_mh_matrix(stream_only=False):
     if not os.path.exists(HARNESS):
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
     z = np.load(os.path.join(HERE, "wiki_csr.npz"))
     tmp = tempfile.mkdtemp(prefix="golden_mh_")
     try:
-        mm = mh_matrix(tmp, z["off"], z["adj"])
+        mm = None if stream_only else mh_matrix(tmp, z["off"], z["adj"])
         ms = mh_stream_matrix(tmp, z["off"], z["adj"])
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     path = os.path.join(HERE, "golden.json")
     meta = json.load(open(path))
-    meta["mh_matrix_reference"] = mm
+    if mm is not None:
+        meta["mh_matrix_reference"] = mm
     meta["mh_stream_matrix_reference"] = ms
     with open(path, "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
@@ -369,4 +417,8 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(main_mh_matrix() if sys.argv[1:] == ["mh-matrix"] else main())
+    if sys.argv[1:] == ["mh-matrix"]:
+        sys.exit(main_mh_matrix())
+    if sys.argv[1:] == ["mh-stream"]:
+        sys.exit(main_mh_matrix(stream_only=True))
+    sys.exit(main())

@@ -77,12 +77,58 @@ def check_cell(ref_cell: dict, ours: np.ndarray, label: str) -> list[str]:
     return bad
 
 
-def stream_batches(matrix: dict, n: int, seed: int, gen_batch):
-    """The (insert?, pairs) batches of mh_stream_matrix_reference for one seed;
+def wiki_compact(off: np.ndarray, adj: np.ndarray):
+    """wiki-graph without its isolated vertices, ids renumbered in order: the
+    graph of the directed stream cells.  A directed batch edge into an isolated
+    vertex makes a sink, where the reference evaluates lrand() % 0
+    (utility.h:220, via node2vec.h:97-105) and dies of SIGFPE."""
+    off = off.astype(np.int64)
+    deg = np.diff(off)
+    keep = np.nonzero(deg > 0)[0]
+    remap = np.full(len(deg), -1, dtype=np.int64)
+    remap[keep] = np.arange(len(keep))
+    src = remap[np.repeat(np.arange(len(deg)), deg)]
+    tgt = remap[adj.astype(np.int64)]
+    n2 = len(keep)
+    off2 = np.zeros(n2 + 1, dtype=np.uint64)
+    np.cumsum(np.bincount(src, minlength=n2), out=off2[1:])
+    return off2, tgt.astype(np.uint32)
+
+
+def stream_batch_seeds(off: np.ndarray, adj: np.ndarray, count: int, edges: int):
+    """The first `count` batch seeds b = 1, 2, ... whose directed batch
+    generate_batch_of_edges(edges, n, b, false, true), inserted and then
+    deleted, leaves every vertex with an out-edge (a vertex left without one
+    would crash the reference, see wiki_compact)."""
+    from oracle import oracle as O
+    off = off.astype(np.int64)
+    n = len(off) - 1
+    deg = np.diff(off)
+    src = np.repeat(np.arange(n, dtype=np.int64), deg)
+    ekeys = src * n + adj.astype(np.int64)
+    out, b = [], 0
+    while len(out) < count:
+        b += 1
+        e = O.generate_batch_of_edges(edges, n, b, False, True).astype(np.int64)
+        # after insert + delete of the same batch every batch edge is gone
+        present = np.isin(e[:, 0] * n + e[:, 1], ekeys)
+        lost = np.bincount(e[present, 0], minlength=n)
+        if not ((deg - lost) == 0).any():
+            out.append(b)
+    return out
+
+
+def stream_batches(cell: dict, i: int, n: int, gen_batch):
+    """The (insert?, pairs) batches of stream cell `cell` for its i-th seed;
     gen_batch = generate_batch_of_edges(edges, n, seed, self_loops, directed)."""
-    return [(b["insert"], gen_batch(b["edges"], n, seed + b["seed_offset"], False, False)) for b in matrix["batches"]]
+    return [(b["insert"], gen_batch(b["edges"], n, b["seed"], False, b["directed"])) for b in cell["batches"][i]]
+
+
+def stream_graph(cell: dict, off: np.ndarray, adj: np.ndarray):
+    """The cell's base graph from wiki's CSR."""
+    return wiki_compact(off, adj) if cell["graph"] == "wiki_compact" else (off, adj)
 
 
 def stream_cells(matrix: dict):
-    return [(k, float(k.split("_")[1][1:]), float(k.split("_")[2][1:]), k.split("_")[3])
-            for k in sorted(matrix) if k.startswith("node2vec_")]
+    """(key, p, q, init name) of every stream cell."""
+    return [(k, c["p"], c["q"], c["init"]) for k, c in sorted(matrix["cells"].items())]

@@ -358,7 +358,11 @@ def test_affected_ids_on_device_match_host_list(W):
 # (WHARF_N2V_REWALK, WHARF_NO_ROW_SLACK, WHARF_POOL_NO_HEADROOM, neighbour filter, WHARF_NO_MEMO,
 #  WHARF_NO_CHUNKED_SCAN, node2vec re-walk start-state table: on / off / 2 buckets, WHARF_NO_PREINIT,
 #  WHARF_NT_ROWS: chunked scans with non-temporal or plain row loads)
+# park/*: the node2vec re-walk by passes (k_rewalk_park + k_park_init), parking until no walker is
+# left (WHARF_PARK_TAIL=0) or finishing a short list with in-wave inits (the default tail)
 PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0", "on", "0", "1"),
+         "park/slack": ("park", "0", "0", "on", "1", "0", "on", "1", "1"),
+         "park/repack-tail": ("park", "1", "1", "off", "0", "1", "tiny", "0", "0"),
          "flat/move": ("flat", "1", "0", "noslack", "0", "0", "off", "0", "0"),
          "sorted/repack": ("sorted", "1", "1", "off", "0", "1", "tiny", "0", "1"),
          "flat/slack-repack": ("flat", "0", "1", "on", "1", "1", "on", "0", "0"),
@@ -393,6 +397,7 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     plain walk-matrix row loads (WHARF_NT_ROWS; the host picks per batch)."""
     n2v_list, no_slack, no_headroom, filt, no_memo, no_chunked, stab, no_pre, nt_rows = PATHS[path]
     monkeypatch.setenv("WHARF_NT_ROWS", nt_rows)
+    monkeypatch.setenv("WHARF_PARK_TAIL", "0" if path == "park/slack" else "8192")
     monkeypatch.setenv("WHARF_NO_PREINIT", no_pre)
     monkeypatch.setenv("WHARF_NO_START_TABLE", "1" if stab == "off" else "0")
     monkeypatch.setenv("WHARF_START_TABLE_BUCKETS", "2" if stab == "tiny" else "0")
@@ -435,6 +440,81 @@ def test_node2vec_anchor_reset_with_prev_row(W, monkeypatch, rows, init):
                (False, O.generate_batch_of_edges(900, 1 << 11, 33, False, False), R | A)]
     _compare_stream(W, off, adj, batches, wpv=4, L=30, model=1, paramP=0.5, paramQ=2.0, sampler_init=init,
                     deterministic=False, seed=4321)
+
+
+@pytest.mark.parametrize("mode", ["det", "node2vec"])
+def test_pool_compaction_without_room_for_a_second_pool(W, monkeypatch, mode):
+    """When the pool runs out of headroom and the device cannot hold a second
+    pool (WHARF_REPACK_MEM_CAP: as if only 1 byte were free), the repack falls
+    back to the in-place compaction: rows keep their capacities and close up the
+    dead slots that moved rows left (node2vec anchors carried along).  Rows
+    without slack move on every growing insert (WHARF_NO_ROW_SLACK=1) and the
+    headroom is 3000 slots, so compactions happen every few batches; corpus,
+    counters, affected ids and CSR stay the oracle's throughout."""
+    monkeypatch.setenv("WHARF_REPACK_MEM_CAP", "1")
+    monkeypatch.setenv("WHARF_NO_ROW_SLACK", "1")
+    monkeypatch.setenv("WHARF_POOL_HEADROOM", "3000")
+    base = O.generate_batch_of_edges(30000, 1 << 12, 17, False, False)
+    off, adj = O.csr_from_edges(1 << 11, base)
+    kw = dict(deterministic=True) if mode == "det" else dict(deterministic=False, seed=77, model=1, paramP=0.5,
+                                                              paramQ=2.0)
+    cfg = W.WharfConfig(walks_per_vertex=3, walk_length=30, **kw)
+    g = W.WharfMH.from_csr(off, adj, config=cfg)
+    ref = O.Engine(off, adj, wpv=3, L=30, model=cfg.model, p=cfg.paramP, q=cfg.paramQ, init=cfg.sampler_init,
+                   deterministic=cfg.deterministic, seed=cfg.seed)
+    g.generate_initial_random_walks()
+    ref.generate()
+    dead_seen = 0
+    for i in range(8):
+        ins = i % 3 != 2
+        b = O.generate_batch_of_edges(700, 1 << 11, 300 + i, False, i % 2 == 1)
+        aff = (g.insert_edges_batch if ins else g.delete_edges_batch)(b, remove_dups=True)
+        np.testing.assert_array_equal(aff, ref.update(ins, b, O.REMOVE_DUPS | O.APPLY_WALK_UPDATES))
+        np.testing.assert_array_equal(g.walks(), ref.walks())
+        o2, a2 = g.flatten_graph()
+        o3, a3 = ref.csr()
+        np.testing.assert_array_equal(o2, o3)
+        np.testing.assert_array_equal(a2, a3)
+        st = g.stats()
+        assert st["steps"] == ref.steps and st["accepts"] == ref.accepts
+        dead_seen = max(dead_seen, st["dead_slots"])
+        assert st["pool_slots"] <= st["pool_capacity"]
+    assert g.stats()["repacks"] >= 1 and dead_seen > 0
+    g.destroy()
+
+
+def test_pool_exhausted_leaves_the_handle_unchanged(W, monkeypatch):
+    """No headroom, no row slack and no memory for a second pool: a growing insert
+    cannot be placed even after the compaction.  It fails with WHARF_E_NOMEM
+    before anything is applied — graph, walks, the update epoch and the sources'
+    sampler epochs (the MH draws of later batches) stay as they were — and the
+    handle goes on: a delete batch afterwards equals the oracle's, which never
+    saw the failed insert."""
+    monkeypatch.setenv("WHARF_REPACK_MEM_CAP", "1")
+    monkeypatch.setenv("WHARF_NO_ROW_SLACK", "1")
+    monkeypatch.setenv("WHARF_POOL_NO_HEADROOM", "1")
+    base = O.generate_batch_of_edges(30000, 1 << 12, 19, False, False)
+    off, adj = O.csr_from_edges(1 << 11, base)
+    cfg = W.WharfConfig(walks_per_vertex=3, walk_length=30, deterministic=False, seed=5, model=1, paramP=0.5,
+                        paramQ=2.0)
+    g = W.WharfMH.from_csr(off, adj, config=cfg)
+    ref = O.Engine(off, adj, wpv=3, L=30, model=1, p=0.5, q=2.0, init=cfg.sampler_init, deterministic=False, seed=5)
+    g.generate_initial_random_walks()
+    ref.generate()
+    w0 = g.walks()
+    ins = O.generate_batch_of_edges(500, 1 << 11, 41, False, False)
+    with pytest.raises(RuntimeError, match=r"\(-3\).*slot pool exhausted"):
+        g.insert_edges_batch(ins, remove_dups=True)
+    np.testing.assert_array_equal(g.walks(), w0)
+    o2, a2 = g.flatten_graph()
+    np.testing.assert_array_equal(o2, off)
+    np.testing.assert_array_equal(a2, adj)
+    d = O.generate_batch_of_edges(800, 1 << 11, 42, False, False)
+    aff = g.delete_edges_batch(d, remove_dups=True)
+    np.testing.assert_array_equal(aff, ref.update(False, d, O.REMOVE_DUPS | O.APPLY_WALK_UPDATES))
+    np.testing.assert_array_equal(g.walks(), ref.walks())
+    assert g.stats()["accepts"] == ref.accepts
+    g.destroy()
 
 
 # ---------------------------------------------------------------------------
@@ -529,28 +609,31 @@ _STREAM = json.load(open(os.path.join(G, "golden.json")))["mh_stream_matrix_refe
 
 @pytest.mark.parametrize("cell", mh_stats.stream_cells(_STREAM), ids=lambda c: c[0])
 def test_mh_stream_vs_reference(W, cell):
-    """MH re-walks through an insert and a delete batch on wiki (the reference's
-    MH update path, wharfmh.h:439-923, sampler resets of batch sources): class
+    """MH re-walks through an insert and a delete batch (the reference's MH
+    update path, wharfmh.h:439-923, sampler resets of batch sources): class
     fractions of the final corpus on the final graph against the reference's 8
-    seeds (`mh_stream_matrix_reference`); the first seed also bit-exact against
-    the oracle."""
+    seeds (`mh_stream_matrix_reference`), for undirected RMAT batches on wiki and
+    for the directed insert/delete pairs of one batch of the reference's driver
+    (throughput-latency.cpp:121,126,135) on wiki without isolated vertices; the
+    first seed also bit-exact against the oracle."""
     key, p, q, init = cell
+    c = _STREAM["cells"][key]
     z = np.load(os.path.join(G, "wiki_csr.npz"))
-    off, adj = z["off"], z["adj"]
+    off, adj = mh_stats.stream_graph(c, z["off"], z["adj"])
     n = len(off) - 1
     inits = {"random": 0, "burnin": 1, "weight": 2}
     ours = []
-    for s in _STREAM["seeds"]:
+    for i, s in enumerate(_STREAM["seeds"]):
         cfg = W.WharfConfig(walks_per_vertex=_STREAM["wpv"], walk_length=_STREAM["L"], model=W.NODE2VEC,
                             paramP=p, paramQ=q, sampler_init=inits[init], deterministic=False, seed=s)
         g = W.WharfMH.from_csr(off, adj, config=cfg)
         g.generate_initial_random_walks()
-        batches = mh_stats.stream_batches(_STREAM, n, s, O.generate_batch_of_edges)
+        batches = mh_stats.stream_batches(c, i, n, O.generate_batch_of_edges)
         for ins, b in batches:
             (g.insert_edges_batch if ins else g.delete_edges_batch)(b, remove_dups=True)
         o2, a2 = g.flatten_graph()
         w = g.walks()
-        if s == _STREAM["seeds"][0]:
+        if i == 0:
             ref = O.Engine(off, adj, wpv=_STREAM["wpv"], L=_STREAM["L"], model=O.NODE2VEC, p=p, q=q,
                            init=inits[init], deterministic=False, seed=s)
             ref.generate()
@@ -559,7 +642,7 @@ def test_mh_stream_vs_reference(W, cell):
             np.testing.assert_array_equal(w, ref.walks())
         ours.append(mh_stats.class_fractions(w, o2, a2))
         g.destroy()
-    bad = mh_stats.check_cell(_STREAM[key], np.array(ours), key)
+    bad = mh_stats.check_cell(c, np.array(ours), key)
     assert not bad, bad
 
 

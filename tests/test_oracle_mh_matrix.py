@@ -52,22 +52,35 @@ def test_oracle_mh_cell_vs_reference(wiki, cell):
 STREAM = json.load(open(os.path.join(G, "golden.json")))["mh_stream_matrix_reference"]
 
 
+def test_stream_matrix_covers_directed_and_undirected_cells():
+    cells = STREAM["cells"]
+    assert len(cells) == 18                       # 3 (p, q) x 3 inits x {undirected, directed}
+    assert sum(c["directed"] for c in cells.values()) == 9
+    for c in cells.values():
+        assert len(c["return"]["per_seed"]) == len(STREAM["seeds"]) == len(c["batches"]) == 8
+
+
 @pytest.mark.parametrize("cell", S.stream_cells(STREAM), ids=lambda c: c[0])
 def test_oracle_mh_stream_vs_reference(wiki, cell):
     """After an insert and a delete batch (re-walks, sampler resets of batch
     sources): class fractions of the final corpus on the final graph, against
-    the reference's 8 seeds (`mh_stream_matrix_reference`)."""
+    the reference's 8 seeds (`mh_stream_matrix_reference`).  Undirected RMAT
+    batches on wiki, and the reference driver's directed insert/delete pairs of
+    one batch (throughput-latency.cpp:121,126,135) on wiki without isolated
+    vertices — the batches where the prev-row anchor reset of DESIGN.md §4
+    departs from the reference's keep-first-anchor samplers."""
     key, p, q, init = cell
-    off, adj = wiki
+    c = STREAM["cells"][key]
+    off, adj = S.stream_graph(c, *wiki)
     n = len(off) - 1
     ours = []
-    for s in STREAM["seeds"]:
+    for i, s in enumerate(STREAM["seeds"]):
         e = O.Engine(off, adj, wpv=STREAM["wpv"], L=STREAM["L"], model=O.NODE2VEC, p=p, q=q, init=INITS[init],
                      deterministic=False, seed=s)
         e.generate()
-        for ins, b in S.stream_batches(STREAM, n, s, O.generate_batch_of_edges):
+        for ins, b in S.stream_batches(c, i, n, O.generate_batch_of_edges):
             e.update(ins, b)
         o2, a2 = e.csr()
         ours.append(S.class_fractions(e.walks(), o2, a2))
-    bad = S.check_cell(STREAM[key], np.array(ours), key)
+    bad = S.check_cell(c, np.array(ours), key)
     assert not bad, bad

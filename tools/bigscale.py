@@ -65,6 +65,7 @@ def main():
         g.set_shard(lo, hi)
         print(f"shard 0 of {a.shard}: start vertices [{lo}, {hi}), {g.number_of_walks} walks", flush=True)
     g.generate_initial_random_walks()
+    first_ms, first_inits = g.stats()["last_walk_kernel_ms"], g.stats()["last_anchor_inits"]
     g.generate_initial_random_walks()
     st = g.stats()
     lo, hi = g.shard()[:2]
@@ -72,7 +73,8 @@ def main():
     ok_steps = st["steps"] == active * 79
     gen_rate = st["steps"] / st["last_walk_kernel_ms"] / 1e6
     print(f"generate: {st['last_walk_kernel_ms']:.1f} ms, steps {st['steps']} (expected {active * 79}), "
-          f"{gen_rate:.2f} G steps/s, accepts {st['accepts']}", flush=True)
+          f"{gen_rate:.2f} G steps/s, accepts {st['accepts']} (first generation {first_ms:.1f} ms, "
+          f"anchor inits {first_inits})", flush=True)
     mem = g.memory_footprint(verbose=False)
     free, total = torch.cuda.mem_get_info(0)
     print(f"device bytes: {json.dumps(mem)}; hipMemGetInfo free {free / 2**30:.1f} of {total / 2**30:.1f} GiB",
@@ -101,7 +103,7 @@ def main():
         del ref
     del off, adj, deg
     out = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device="cuda:0")
-    lat, gms, wms, affs, steps = [], [], [], [], []
+    lat, gms, wms, affs, steps, inits, passes = [], [], [], [], [], [], []
     for b in range(a.batches):
         batch = W.generate_batch_of_edges(5000, n, b, False, False)
         for ins in ((True, False) if a.mixed else (True,)):
@@ -113,8 +115,10 @@ def main():
             wms.append(s2["last_walk_update_ms"])
             affs.append(len(aff))
             steps.append(s2["steps"])
+            inits.append(s2["last_anchor_inits"])
+            passes.append(s2["last_rewalk_passes"])
         print(f"batch {b}: {lat[-1]:.1f} ms (graph {gms[-1]:.1f}, re-walk {wms[-1]:.1f}), affected {affs[-1]}, "
-              f"m {g.number_of_edges()}", flush=True)
+              f"steps {steps[-1]}, anchor inits {inits[-1]}, passes {passes[-1]}, m {g.number_of_edges()}", flush=True)
         if b == 0:
             m1 = g.memory_footprint(verbose=False)
             free, _ = torch.cuda.mem_get_info(0)
@@ -132,12 +136,15 @@ def main():
                      "generate_batch_of_edges(5000, n, b, false, false)",
            "n": n, "m": m, "walks": g.number_of_walks, "shard_of": a.shard, "build_s": round(t_build, 1),
            "gen_ms": round(st["last_walk_kernel_ms"], 2), "gen_Gsteps_per_s": round(gen_rate, 2),
+           "first_gen_ms": round(first_ms, 2), "first_gen_anchor_inits": first_inits,
            "steps_ok": ok_steps, "bad_transitions": bad, "oracle_window_identical": same,
            "batch_median_ms": round(float(np.median(lat)), 2), "batch_p90_ms": round(float(np.percentile(lat, 90)), 2),
            "graph_update_median_ms": round(float(np.median(gms)), 2),
            "walk_update_median_ms": round(float(np.median(wms)), 2),
            "mean_affected": int(np.mean(affs)),
            "rewalk_Gsteps_per_s": round(float(np.sum(steps) / np.sum(wms) / 1e6), 2),
+           "mean_rewalk_steps": int(np.mean(steps)), "mean_anchor_inits": int(np.mean(inits)),
+           "rewalk_passes": passes,
            "m_after_batches": m2, "pool_slots": pst["pool_slots"], "pool_capacity": pst["pool_capacity"],
            "repacks": pst["repacks"], "m_after_delete_last": m3, "device_bytes_total": mem["total_bytes"]}
     print(json.dumps(res), flush=True)
