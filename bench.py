@@ -23,8 +23,12 @@ that the headline.
 
 Sub-records on rank 0 (same run): `mh_node2vec` (configs[4]'s model, p=.5
 q=2 WEIGHT, on the configs[1] graph: first and warm generation, a configs[2]
-re-walk stream), `rewalk_latency_10k_batch[_deterministic]` (configs[2]) and
-`streaming_rooflines` (rewalk-point scan, deterministic suffix copy, CSR move).
+re-walk stream), `rewalk_latency_10k_batch[_deterministic]` (configs[2]),
+`streaming_rooflines` (rewalk-point scan, deterministic suffix copy, CSR move)
+and `per_gpu_of_8`: the per-GPU work of configs[3] and configs[4] on 8 GPUs
+(full graph, walk shard 0 of 8) run on this GPU, with configs[3]'s all-walks
+1-GPU time beside it.  The box's random-gather rate is probed 3 times before the
+timed region (`roofline.gather_ceiling`).
 """
 from __future__ import annotations
 
@@ -79,6 +83,10 @@ def parse():
     p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     p.add_argument("--n2v-steps", type=int, default=3, help="node2vec warm generations of the mh_node2vec record (0 = off)")
     p.add_argument("--n2v-rewalk-batches", type=int, default=5, help="configs[2] batches of the mh_node2vec record")
+    p.add_argument("--gather-probes", type=int, default=3, help="tools/gather_roof runs before the timed region")
+    p.add_argument("--per-gpu-of-8", type=int, default=1,
+                   help="configs[3] / configs[4]: the per-GPU work of their 8-GPU runs on this GPU (0 = off)")
+    p.add_argument("--per8-batches", type=int, default=5, help="update batches per per_gpu_of_8 case")
     return p.parse_args()
 
 
@@ -87,36 +95,39 @@ def balanced_shards(deg: np.ndarray, parts: int):
     return bs(deg, parts)
 
 
-def measure_gather_ceiling():
-    """The chip's dependent random 16-B gather rate with the walk kernel's shape,
-    measured on this box by tools/gather_roof (boxes differ by up to ~10 %);
-    None when the probe is not built."""
+def measure_gather_ceiling(runs: int = 3):
+    """The chip's dependent random 16-B gather rate with the walk kernel's shape
+    (41.9 M lanes x 79 dependent gathers from a 3.5 GiB table), measured on this
+    box by tools/gather_roof `runs` times BEFORE the timed region, on an idle
+    GPU (boxes differ by up to ~10 %; round 2 probed after ~55 s of load and got
+    a rate the kernel then beat by 10 %).  None when the probe is not built."""
     exe = os.path.join(REPO, "tools", "gather_roof")
     if not os.access(exe, os.X_OK):
         return None
-    try:
-        r = subprocess.run([exe, "3.48", "coarse", "dep"], capture_output=True, text=True, timeout=180)
-        for line in r.stdout.splitlines():
-            if line.startswith("{"):
-                return float(json.loads(line)["Ggathers_per_s"])
-    except (subprocess.SubprocessError, ValueError, KeyError, OSError):
-        pass
-    return None
+    rates = []
+    for _ in range(runs):
+        try:
+            r = subprocess.run([exe, "3.48", "coarse", "dep"], capture_output=True, text=True, timeout=180)
+            for line in r.stdout.splitlines():
+                if line.startswith("{"):
+                    rates.append(float(json.loads(line)["Ggathers_per_s"]))
+        except (subprocess.SubprocessError, ValueError, KeyError, OSError):
+            pass
+    return rates or None
 
 
-def gather_ceiling(steps_per_s: float, live: float | None):
-    """The kernel's binding ceiling: one dependent random 16-B gather per step,
-    at the random-gather rate measured live on this box (else the committed
-    measurement of another box, profiles/gather_ceiling.json)."""
-    if live:
-        return {"Ggathers_per_s": round(live, 2), "frac": round(steps_per_s / (live * 1e9), 4),
-                "source": "tools/gather_roof dep, this box"}
-    path = os.path.join(REPO, "profiles", "gather_ceiling.json")
-    if not os.path.exists(path):
+def gather_ceiling(steps_per_s: float, live):
+    """The generation kernel against the box's random-gather rate (one dependent
+    16-B gather per step), probed before the timed region: min / max of the
+    probes and the kernel's rate as a fraction of each.  A fraction above 1 is
+    probe noise, not headroom: the probe is a yardstick for the box, the
+    roofline is `roofline.frac`."""
+    if not live:
         return None
-    g = json.load(open(path))
-    return {"Ggathers_per_s": g["Ggathers_per_s"], "frac": round(steps_per_s / (g["Ggathers_per_s"] * 1e9), 4),
-            "source": "profiles/gather_ceiling.json (another box)"}
+    lo, hi = min(live), max(live)
+    return {"Ggathers_per_s_min": round(lo, 2), "Ggathers_per_s_max": round(hi, 2), "probes": [round(x, 2) for x in live],
+            "frac_of_min": round(steps_per_s / (lo * 1e9), 4), "frac_of_max": round(steps_per_s / (hi * 1e9), 4),
+            "source": "tools/gather_roof 3.48 coarse dep, this box, before the timed region"}
 
 
 PMC_ROUNDS = ("r02_", "")   # newest round's rocprofv3 summary first
@@ -136,12 +147,34 @@ def load_traffic(tag: str):
     return None, None
 
 
-def cpu_cores(requested: int) -> int:
+def host_cpus():
+    """What the host gives this job: nproc, the affinity set, the cgroup CPU
+    quota (a GPU box shows the whole machine's CPUs but grants a share), the
+    CPU model."""
+    info = {"nproc": os.cpu_count()}
     try:
-        avail = len(os.sched_getaffinity(0))
+        info["affinity"] = len(os.sched_getaffinity(0))
     except Exception:
-        avail = os.cpu_count() or 1
-    return max(1, min(requested or 16, avail))
+        info["affinity"] = info["nproc"]
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    info["cgroup_cpu_quota"] = quota
+    try:
+        info["model"] = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except Exception:
+        info["model"] = None
+    info["usable"] = max(1, min(info["affinity"] or 1, quota or info["affinity"] or 1))
+    return info
+
+
+def cpu_cores(requested: int) -> int:
+    """Every host core this job may use (affinity, capped by the cgroup quota), unless --cpu-threads."""
+    return requested if requested > 0 else host_cpus()["usable"]
 
 
 def cpu_baseline(args, n, active_vertices, off, adj, kind):
@@ -163,12 +196,15 @@ def cpu_baseline(args, n, active_vertices, off, adj, kind):
             if r.returncode == 0 and m:
                 secs = float(m.group(1))
                 steps = active_vertices * (args.cpu_length - 1)
+                full = active_vertices * args.wpv * (args.length - 1)
                 return {"value": steps / secs, "unit": "walk-steps/s", "cores": cores, "kind": "reference",
                         "sample": f"reference WharfMH::generate_initial_random_walks on the same RMAT graph "
                                   f"(n={n}), walks_per_vertex=1 (1/{args.wpv} of the workload), L={args.cpu_length} "
                                   f"(workload: {args.length}), "
                                   f"{'deterministic' if args.det else 'MH'} {args.model}; {steps} steps in {secs:.2f} s",
-                        "seconds": secs}
+                        "seconds": secs, "host": host_cpus(),
+                        "full_workload_steps": full,
+                        "full_workload_seconds_extrapolated": round(full / (steps / secs), 1)}
             log("cpu_baseline: harness failed", r.returncode, r.stderr[-500:])
         except subprocess.TimeoutExpired:
             log("cpu_baseline: harness timed out")
@@ -181,9 +217,11 @@ def cpu_baseline(args, n, active_vertices, off, adj, kind):
     w1 = min(n * args.wpv, 2_000_000)
     secs = eng.time_generate_range(0, w1, cores)
     steps = eng.steps
+    full = active_vertices * args.wpv * (args.length - 1)
     return {"value": steps / secs, "unit": "walk-steps/s", "cores": cores, "kind": "port",
             "sample": f"oracle/wharf_oracle.c restatement, same graph, walks [0, {w1}), L={args.length}; "
-                      f"{steps} steps in {secs:.2f} s", "seconds": secs}
+                      f"{steps} steps in {secs:.2f} s", "seconds": secs, "host": host_cpus(),
+            "full_workload_steps": full, "full_workload_seconds_extrapolated": round(full / (steps / secs), 1)}
 
 
 def cpu_baseline_deterministic(args, batches=3):
@@ -213,14 +251,17 @@ def cpu_baseline_deterministic(args, batches=3):
     if r.returncode != 0 or not gen or not upd:
         log("cpu_baseline_deterministic: harness failed", r.returncode, r.stderr[-500:])
         return None
-    return {"kind": "reference", "cores": cores,
+    return {"kind": "reference", "cores": cores, "host": host_cpus(),
             "sample": f"reference WharfMH, deterministic mode, configs[2]'s graph (RMAT scale {args.scale}, "
                       f"{args.stream_samples} undirected samples), walks_per_vertex=1, L={args.cpu_length} "
                       f"(the GPU line: {args.wpv} x {args.length}); {batches} insert batches of "
                       f"generate_batch_of_edges(5000, n, b, false, undirected), walk update applied",
             "generation_seconds": float(gen.group(1)),
             "insert_batch_median_ms": round(float(np.median([u[0] for u in upd])) * 1e3, 1),
-            "mean_affected_walks": int(np.mean([u[1] for u in upd]))}
+            "mean_affected_walks": int(np.mean([u[1] for u in upd])),
+            # the walk update re-walks ~(walks x remaining length): scaled linearly to the GPU line's wpv and L
+            "insert_batch_ms_extrapolated_to_workload": round(float(np.median([u[0] for u in upd])) * 1e3 * args.wpv
+                                                              * (args.length - 1) / (args.cpu_length - 1), 1)}
 
 
 def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrier, batches, scan_batches=0):
@@ -343,6 +384,15 @@ def node2vec_record(args, W, torch, dev, barrier, n):
     avg = float(np.mean(kern))
     achieved = steps * BYTES_PER_STEP_NODE2VEC / (avg * 1e-3) / 1e9
     n2v_traffic, n2v_traffic_src = load_traffic(f"gen_node2vec_mh_s{args.scale}")
+    # SURVEY 8(d)'s node2vec unit prices the reference's has_edge binary search in
+    # prev's row: 44 + 4 * ceil(log2 deg(prev)) B per step, with the mean probe
+    # count measured over the transitions of 4096 walks of this corpus
+    deg = np.diff(g.offsets().astype(np.int64))
+    w0 = (g.number_of_walks // 2) & ~0xFFFF
+    prevs = np.concatenate([g.walk_vertices(w0 + i)[:-1] for i in range(4096)]).astype(np.int64)
+    probes = float(np.mean(np.ceil(np.log2(np.maximum(deg[prevs], 1)))))
+    survey_bps = 44 + 4 * probes
+    survey_achieved = steps * survey_bps / (avg * 1e-3) / 1e9
     rec = {"workload": f"configs[1] graph (RMAT scale {args.scale}, m={g.number_of_edges()}), node2vec "
                        f"p={args.paramP} q={args.paramQ} MH, WEIGHT sampler init, walks_per_vertex={args.wpv}, "
                        f"walk_length={args.length}",
@@ -353,6 +403,14 @@ def node2vec_record(args, W, torch, dev, barrier, n):
            "roofline": {"bound": "hbm", "kernel": "k_walk<node2vec, MH> (warm generation)",
                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "bytes_per_step": BYTES_PER_STEP_NODE2VEC,
+                        "bytes_per_step_basis": "as built: 32-B edge record with the anchor entry + one 32-B edge-hash "
+                                                "bucket + 4-B output",
+                        "survey_unit": {"bytes_per_step": round(survey_bps, 2),
+                                        "mean_binary_search_probes": round(probes, 3),
+                                        "formula": "44 + 4 * ceil(log2 deg(prev)) (SURVEY 8(d)), probes measured over "
+                                                   "the transitions of 4096 walks",
+                                        "achieved": round(survey_achieved, 2),
+                                        "frac": round(survey_achieved / HBM_PEAK_GBS, 5)},
                         "traffic": n2v_traffic, "traffic_source": n2v_traffic_src}}
     g.destroy()
     rec["rewalk_latency_10k_batch"] = stream_latency(args, W, torch, cfg, dev, 1, 0, None, None, barrier,
@@ -397,6 +455,97 @@ def streaming_rooflines(rewalk, rewalk_det, scale):
     return out or None
 
 
+def _update_stream(g, W, n, batches, mixed, out):
+    """Insert batch b (and, mixed, delete it again: throughput-latency.cpp:126,135)
+    for b < batches: generate_batch_of_edges(5000, n, b, false, undirected)
+    (memory-throughput-latency.cpp:126-134).  Per-update device times."""
+    rec = {k: [] for k in ("ms", "graph_ms", "walk_ms", "kernel_ms", "in_edge_ms", "steps", "affected", "inits")}
+    for b in range(batches):
+        batch = W.generate_batch_of_edges(5000, n, b, False, False)
+        for ins in ((True, False) if mixed else (True,)):
+            t1 = time.perf_counter()
+            (g.insert_edges_batch if ins else g.delete_edges_batch)(batch, remove_dups=True, out=out)
+            rec["ms"].append((time.perf_counter() - t1) * 1e3)
+            st = g.stats()
+            rec["graph_ms"].append(st["last_graph_update_ms"])
+            rec["walk_ms"].append(st["last_walk_update_ms"])
+            rec["kernel_ms"].append(st["last_walk_kernel_ms"])
+            rec["in_edge_ms"].append(st["last_csr_move_ms"])
+            rec["steps"].append(st["steps"])
+            rec["affected"].append(st["affected"])
+            rec["inits"].append(st["last_anchor_inits"])
+    med = lambda k: round(float(np.median(rec[k])), 3)
+    return {"updates": len(rec["ms"]), "batch_median_ms": med("ms"), "batch_p90_ms": round(float(np.percentile(rec["ms"], 90)), 3),
+            "graph_update_median_ms": med("graph_ms"), "walk_update_median_ms": med("walk_ms"),
+            "rewalk_kernel_median_ms": med("kernel_ms"), "in_edge_scan_median_ms": round(float(np.median(rec["in_edge_ms"])), 4),
+            "mean_affected_walks": int(np.mean(rec["affected"])), "mean_rewalk_steps": int(np.mean(rec["steps"])),
+            "rewalk_Gsteps_per_s": round(float(np.sum(rec["steps"]) / np.sum(rec["walk_ms"]) / 1e6), 2),
+            "mean_anchor_inits": int(np.mean(rec["inits"]))}
+
+
+def per_gpu_of_8(args, W, torch, dev, barrier):
+    """The per-GPU work of BASELINE configs[3] and configs[4] on 8 GPUs, run on
+    this one GPU: the full graph (replicated on every rank, wharfmh.h:275,761
+    shard by walk) with the walks of start-vertex shard 0 of 8.  configs[3]:
+    twitter-sized RMAT (scale 25, 1.2 G undirected samples), DeepWalk wpv 10,
+    insert batches, MH and deterministic; beside it the same graph with every
+    walk on this one GPU (the 1-GPU time an 8-GPU run divides).  configs[4]:
+    friendster-sized RMAT (scale 26, 1.8 G samples), node2vec p=.5 q=2 MH WEIGHT,
+    wpv 10 (the survey's 656 M walks / 8), mixed insert/delete batches.  The
+    graphs use seed 4 (tools/bigscale.py).  Each case is skipped with its error
+    when the device cannot hold it, so the headline line always prints."""
+    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards
+    out = {"note": "one GPU running the work one rank of an 8-GPU job does; graphs built on the device (seed 4)"}
+    cases = [("configs3_deepwalk_mh_shard0of8", 25, 1_200_000_000, W.DEEPWALK, False, 8, False),
+             ("configs3_deepwalk_det_shard0of8", 25, 1_200_000_000, W.DEEPWALK, True, 8, False),
+             ("configs3_deepwalk_mh_all_walks_1gpu", 25, 1_200_000_000, W.DEEPWALK, False, 1, False),
+             ("configs4_node2vec_mh_shard0of8", 26, 1_800_000_000, W.NODE2VEC, False, 8, True)]
+    for name, scale, samples, model, det, parts, mixed in cases:
+        n = 1 << scale
+        g = None
+        try:
+            t0 = time.time()
+            cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, model=model, paramP=0.5, paramQ=2.0,
+                                deterministic=det, seed=0x5EED)
+            g = W.WharfMH.from_rmat(n, samples, 2 * n, seed=4, config=cfg, device=dev)
+            deg = np.diff(g.offsets().astype(np.int64))
+            lo, hi = balanced_shards(deg, parts)[0]
+            g.set_shard(lo, hi)
+            build_s = time.time() - t0
+            g.generate_initial_random_walks()
+            first = g.stats()
+            g.generate_initial_random_walks()
+            warm = g.stats()
+            ids = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
+            barrier()
+            rec = {"graph": f"RMAT scale {scale}, {samples} undirected samples (seed 4), m={g.number_of_edges()}",
+                   "model": f"{'node2vec p=0.5 q=2 WEIGHT' if model == W.NODE2VEC else 'DeepWalk'} "
+                            f"{'deterministic' if det else 'MH'}, walks_per_vertex=10, L=80",
+                   "walks": g.number_of_walks, "shard": [int(lo), int(hi)], "of": parts, "build_s": round(build_s, 1),
+                   "first_generation_ms": round(first["last_walk_kernel_ms"], 2),
+                   "first_generation_anchor_inits": first["last_anchor_inits"],
+                   "generation_ms": round(warm["last_walk_kernel_ms"], 2),
+                   "generation_Gsteps_per_s": round(warm["steps"] / warm["last_walk_kernel_ms"] / 1e6, 2),
+                   "batches": f"{args.per8_batches} x generate_batch_of_edges(5000, n, b, false, undirected)"
+                              f"{', each inserted then deleted' if mixed else ', inserted'}",
+                   "device_bytes": g.memory_footprint(verbose=False)["total_bytes"]}
+            rec.update(_update_stream(g, W, n, args.per8_batches, mixed, ids))
+            out[name] = rec
+            log(f"per_gpu_of_8 {name}: {json.dumps(rec)}")
+        except Exception as ex:   # noqa: BLE001 (a case that does not fit is reported, not fatal)
+            out[name] = {"error": str(ex)[:500]}
+            log(f"per_gpu_of_8 {name} failed: {ex}")
+        finally:
+            if g is not None:
+                g.destroy()
+            torch.cuda.empty_cache()
+    a, b = out.get("configs3_deepwalk_mh_shard0of8", {}), out.get("configs3_deepwalk_mh_all_walks_1gpu", {})
+    if "batch_median_ms" in a and "batch_median_ms" in b:
+        out["configs3_batch_speedup_1gpu_to_shard"] = round(b["batch_median_ms"] / a["batch_median_ms"], 2)
+        out["configs3_generation_speedup_1gpu_to_shard"] = round(b["generation_ms"] / a["generation_ms"], 2)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -417,6 +566,11 @@ def main():
         else:
             dist.init_process_group(backend)
     import dynamicgraphrepresentationlearning_amd as W
+
+    # the box's random-gather rate, probed on the idle GPU before anything is timed
+    live_ceiling = measure_gather_ceiling(args.gather_probes) if rank == 0 and args.gather_probes > 0 else None
+    if live_ceiling:
+        log(f"gather_roof probes (G gathers/s): {live_ceiling}")
 
     # weak scaling: configs[1]'s graph, 10 x N walks per vertex, so each rank's
     # start-vertex range carries configs[1]'s 41.9 M walks
@@ -507,11 +661,15 @@ def main():
     if world == 1 and args.model == "deepwalk" and not args.det and args.n2v_steps > 0:
         n2v = node2vec_record(args, W, torch, dev, barrier, n)
 
+    per8 = None
+    if world == 1 and args.per_gpu_of_8 and args.model == "deepwalk" and not args.det:
+        torch.cuda.empty_cache()
+        per8 = per_gpu_of_8(args, W, torch, dev, barrier)
+
     if rank == 0:
-        live_ceiling = measure_gather_ceiling() if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None
-        if rewalk and live_ceiling:
-            # re-walk steps (one gather each) against the same ceiling; the scan rides along
-            rewalk["rewalk_frac_of_gather_ceiling"] = round(rewalk["rewalk_Gsteps_per_s"] / live_ceiling, 4)
+        if rewalk and live_ceiling and bytes_per_step == BYTES_PER_STEP_DEEPWALK:
+            # re-walk steps (one gather each) against the same yardstick; the scan rides along
+            rewalk["rewalk_frac_of_gather_ceiling_min"] = round(rewalk["rewalk_Gsteps_per_s"] / min(live_ceiling), 4)
         achieved = (steps_local * bytes_per_step / (avg_kernel_ms * 1e-3) / 1e9) if bytes_per_step else None
         traffic, traffic_src = load_traffic(tag)
         line = {
@@ -545,6 +703,7 @@ def main():
                          "first_generation_kernel_ms": round(warm_ms[0], 3) if warm_ms else None,
                          "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3), live_ceiling)
                          if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None},
+            "per_gpu_of_8": per8,
             "mh_accept_rate": round(st["accepts"] / st["steps"], 5) if st["steps"] else None,
             "strong_scaling": strong,
             "mh_node2vec": n2v,

@@ -532,6 +532,8 @@ struct wharf_handle {
         a.inv_p = 1.0f / cfg.paramP;   // node2vec.h:81 `1 / this->paramP` in float
         a.inv_q = 1.0f / cfg.paramQ;
         a.model = cfg.model; a.init = cfg.sampler_init; a.det = cfg.deterministic;
+        const char* ns = getenv("WHARF_NO_SURE_SKIP");   // A/B: initialise every uncached anchor a step meets
+        a.no_sure = ns && atoi(ns) ? 1 : 0;
         return a;
     }
 
@@ -796,13 +798,12 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
             pa.runs = h->runs.as<RunInfo>();
             launch_anchor_preinit(pa, preoff, k, s);
         }
-        // node2vec MH re-walk: by passes with batched anchor inits where the walks are sparse in
-        // the states (the cold-cache case: the pre-init rule's `dense` is false), else the
-        // lock-step sorted kernel.  WHARF_N2V_REWALK=park|sorted|flat forces one.
+        // node2vec MH re-walk: the lock-step sorted kernel (k_rewalk_sorted); WHARF_N2V_REWALK=park
+        // runs it by passes with batched anchor inits (k_rewalk_park: 2-3x slower on configs[4]'s
+        // shard, whose re-walk is bound by the init loads themselves, profiles/r03/park_ab),
+        // =flat lanes at their own pace
         const char* rw = getenv("WHARF_N2V_REWALK");
-        const std::string rmode = rw ? rw : "";
-        a.park = a.model == kNode2Vec && !a.det && a.anchor && !a.scan_only &&
-                 (rmode == "park" || (rmode.empty() && !dense));
+        a.park = a.model == kNode2Vec && !a.det && a.anchor && !a.scan_only && rw && std::string(rw) == "park";
         h->walks_changed();
         launch_walk(a, true, s);
         HIPCHK(hipGetLastError());

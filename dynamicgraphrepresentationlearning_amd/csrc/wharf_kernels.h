@@ -55,6 +55,7 @@ struct WalkArgs {
     uint32_t wpv;
     int nt_rows;                 // chunked scans: non-temporal walk-matrix row loads (most walks re-walk)
     int park;                    // node2vec MH re-walk by passes (k_rewalk_park / k_park_init), run by the host
+    int no_sure;                 // A/B: initialise every uncached anchor a step meets (no sure-accept skip)
 };
 
 constexpr uint64_t kListMask = (1ull << 40) - 1;   // counters[2]: tickets << 40 | re-walk list entries

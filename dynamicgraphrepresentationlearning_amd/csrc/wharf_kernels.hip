@@ -299,20 +299,13 @@ __device__ __forceinline__ void anchor_lookup(const WalkArgs& a, const Row& rc, 
     }
 }
 
-// anchors computed (MH sampler inits): counters[7], one atomic per wave
-__device__ __forceinline__ void count_inits(const WalkArgs& a, bool need)
-{
-    const uint64_t m = __ballot(need);
-    if (m && __lane_id() == (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(a.counters + 7, (unsigned long long)__popcll(m));
-}
-
 // The anchor of a state whose cache entry is empty (need), computed and
 // cached.  Called by every active lane of the wave together (WEIGHT inits are
 // wave-cooperative); lanes with need = false pass an / cls through.
 __device__ __forceinline__ uint32_t anchor_fill(const WalkArgs& a, bool need, const Row& rc, const Row& rp,
-                                                uint64_t* ac, uint64_t anc, uint32_t an, uint32_t& cls)
+                                                uint64_t* ac, uint64_t anc, uint32_t an, uint32_t& cls, uint32_t& inits)
 {
-    count_inits(a, need);
+    inits += need;   // per lane; the kernel adds them up once (counters[7])
     if (a.init == kInitWeight) {
         anchor_init_wave(a, need, rc, rp, an, cls);
     } else if (need) {
@@ -332,15 +325,6 @@ __device__ __forceinline__ uint32_t anchor_fill(const WalkArgs& a, bool need, co
 #endif
     if (need && ac) *ac = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     return an;
-}
-
-__device__ __forceinline__ uint32_t anchor_get(const WalkArgs& a, const Row& rc, const Row& rp, uint64_t* ac,
-                                               uint64_t anc, uint32_t& cls)
-{
-    uint32_t an = 0;
-    bool need;
-    anchor_lookup(a, rc, rp, ac, anc, an, cls, need);
-    return anchor_fill(a, need, rc, rp, ac, anc, an, cls);
 }
 
 // Heaviest weight class (node2vec.h:74-88: 1/p, 1, 1/q) and the lightest a
@@ -385,7 +369,7 @@ __device__ __forceinline__ Row load_edge(const WalkArgs& a, uint64_t e, uint64_t
 template <int MODEL, bool DET, bool PARK = false>
 __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, const uint64_t* __restrict__ rt,
                                               uint32_t pos, uint32_t wlo, uint32_t whi, uint32_t ep, uint32_t& accepts,
-                                              bool* parked = nullptr)
+                                              uint32_t& inits, bool* parked = nullptr)
 {
     Row nx;
     if constexpr (DET) {
@@ -418,7 +402,8 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
             // stays empty for a later walker that needs it).  In the sparse
             // re-walks of configs[4] 79 % of the steps enter a state with no
             // cached anchor; p = .5, q = 2 settles a quarter of them here.
-            const bool sure = need && accept(cand.v == w.rp.v ? a.inv_p : w_lightest_nonreturn(a), w_heaviest(a));
+            const bool sure = need && !a.no_sure &&
+                              accept(cand.v == w.rp.v ? a.inv_p : w_lightest_nonreturn(a), w_heaviest(a));
             const bool init = need && !sure;
             if constexpr (PARK) {
                 if (init) {
@@ -426,7 +411,7 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
                     return 0;
                 }
             } else {
-                ai = anchor_fill(a, init, w.rc, w.rp, w.ac, w.anc, ai, acls);
+                ai = anchor_fill(a, init, w.rc, w.rp, w.ac, w.anc, ai, acls, inits);
             }
             bool ok = true;   // proposing the anchor itself is always accepted
             if (!sure && ai != ci) {
@@ -544,9 +529,9 @@ __device__ __forceinline__ void walk_state(const WalkArgs& a, uint32_t cur, uint
 #define WHARF_PREINIT_ROUNDS 4   // proposals per lane in flight in the pre-init kernels (full waves)
 #endif
 __device__ __forceinline__ void anchor_compute(const WalkArgs& a, bool need, const Row& rc, const Row& rp,
-                                               uint32_t& an, uint32_t& cls)
+                                               uint32_t& an, uint32_t& cls, uint32_t& inits)
 {
-    count_inits(a, need);
+    inits += need;
     if (a.init == kInitWeight) anchor_init_wave<WHARF_PREINIT_ROUNDS>(a, need, rc, rp, an, cls);
     else if (need) an = anchor_init(a, rc, rp, cls);
 }
@@ -555,6 +540,7 @@ __global__ __launch_bounds__(256) void k_anchor_preinit(WalkArgs a, const uint64
 {
     const uint64_t total = preoff[k];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t inits = 0;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
         uint64_t lo = 0, hi = k;   // the source i with preoff[i] <= t < preoff[i + 1]
         while (hi - lo > 1) {
@@ -569,12 +555,12 @@ __global__ __launch_bounds__(256) void k_anchor_preinit(WalkArgs a, const uint64
         uint32_t an = 0, cls = 0;
         // (y, x): entry of slot x -> y (a walker that crosses it and stays at y needs y's row)
         const bool need_a = ry.deg != 0;
-        anchor_compute(a, need_a, ry, rx, an, cls);
+        anchor_compute(a, need_a, ry, rx, an, cls, inits);
         if (need_a) a.anchor[e * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
         // (x, y): entry of slot y -> x, and the start-state table
         const int64_t ein = row_find(a.adj, ry, x);
         const bool need_b = ein >= 0;
-        anchor_compute(a, need_b, rx, ry, an, cls);
+        anchor_compute(a, need_b, rx, ry, an, cls, inits);
         if (need_b) {
             const uint64_t v = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
             a.anchor[(uint64_t)ein * kAnchorStride] = v;
@@ -584,6 +570,7 @@ __global__ __launch_bounds__(256) void k_anchor_preinit(WalkArgs a, const uint64
             }
         }
     }
+    wave_add(a.counters + 7, inits);
 }
 
 // Generation with a cold anchor cache (node2vec MH, the first generation of a
@@ -605,6 +592,7 @@ __global__ void k_slot_owner_marks(const uint64_t* __restrict__ off, const uint3
 __global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint32_t* __restrict__ owner, uint64_t slots)
 {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t inits = 0;
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < slots; e += stride) {
         const uint32_t y = a.adj[e], o = owner[e];
         bool need = y != kGap && o != 0;
@@ -615,9 +603,10 @@ __global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint3
             need = e < rx.off + rx.deg && ry.deg != 0;   // (slots past a row's end are kGap; the test is cheap)
         }
         uint32_t an = 0, cls = 0;
-        anchor_compute(a, need, ry, rx, an, cls);
+        anchor_compute(a, need, ry, rx, an, cls, inits);
         if (need) a.anchor[e * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     }
+    wave_add(a.counters + 7, inits);
 }
 
 void launch_slot_owner_marks(const uint64_t* off, const uint32_t* deg, uint64_t n, uint32_t* owner, hipStream_t s)
@@ -652,7 +641,7 @@ void launch_anchor_preinit(const WalkArgs& a, const uint64_t* preoff, uint64_t k
 template <int MODEL, bool DET>
 __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
 {
-    uint32_t steps = 0, accepts = 0;
+    uint32_t steps = 0, accepts = 0, inits = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t* __restrict__ walks = a.walks;
     const uint64_t W = a.W;
@@ -668,13 +657,14 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
         uint32_t pos = 0;
         for (; pos + 1 < a.L; pos++) {
             if (w.rc.deg == 0) break;   // dead end: the walk stops (reference: lrand() % 0)
-            walks[(uint64_t)(pos + 1) * W + li] = walk_step<MODEL, DET>(a, w, rt, pos, wlo, whi, ep, accepts);
+            walks[(uint64_t)(pos + 1) * W + li] = walk_step<MODEL, DET>(a, w, rt, pos, wlo, whi, ep, accepts, inits);
             steps++;
         }
         for (pos = pos + 1; pos < a.L; pos++) walks[(uint64_t)pos * W + li] = kSent;
     }
     wave_add(a.counters + 0, steps);
     wave_add(a.counters + 1, accepts);
+    wave_add(a.counters + 7, inits);
 }
 
 // Fused rewalk-point scan + suffix re-walk (wharfmh.h:519-537 + 761-859),
@@ -714,7 +704,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
 {
     __shared__ uint32_t s_bloom[kBloomWords];
     bloom_to_lds(a, s_bloom);
-    uint32_t steps = 0, accepts = 0;
+    uint32_t steps = 0, accepts = 0, inits = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t* __restrict__ walks = a.walks;
     const uint64_t W = a.W;
@@ -735,7 +725,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
             bool fresh = false;
             if (mode == kLaneWalk) {
                 if (w.rc.deg) {
-                    val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts);
+                    val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
                     steps++;
                 }
                 fresh = true;
@@ -765,6 +755,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
     }
     wave_add(a.counters + 0, steps);
     wave_add(a.counters + 1, accepts);
+    wave_add(a.counters + 7, inits);
 }
 
 // Deterministic re-walk by suffix table.  In deterministic mode a re-walk
@@ -793,7 +784,7 @@ __global__ __launch_bounds__(256) void k_det_suffix(WalkArgs a)
         uint32_t unused = 0;
         for (uint32_t j = 1; j < a.memo_stride; j++) {
             uint32_t val = kSent;
-            if (j < a.L && w.rc.deg) val = walk_step<kDeepWalk, true>(a, w, rt, j - 1, 0, 0, 0, unused);
+            if (j < a.L && w.rc.deg) val = walk_step<kDeepWalk, true>(a, w, rt, j - 1, 0, 0, 0, unused, unused);
             out[j] = val;
         }
     }
@@ -1190,7 +1181,7 @@ __global__ __launch_bounds__(256) WHARF_SCAN_WAVES void k_rewalk_plan(WalkArgs a
 template <int MODEL, bool DET>
 __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
 {
-    uint32_t steps = 0, accepts = 0;
+    uint32_t steps = 0, accepts = 0, inits = 0;
     uint32_t* __restrict__ walks = a.walks;
     const uint64_t W = a.W, cnt = a.counters[2] & kListMask;
     const uint32_t L = a.L, ep = a.epoch << 4;
@@ -1223,7 +1214,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
         for (uint32_t pos = first; pos < L; pos++) {
             uint32_t val = kSent;
             if (active && pos > p && w.rc.deg) {
-                val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts);
+                val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
                 steps++;
             }
             // the lanes are walks scattered over a block (sorted by rewalk point),
@@ -1238,6 +1229,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
     }
     wave_add(a.counters + 0, steps);
     wave_add(a.counters + 1, accepts);
+    wave_add(a.counters + 7, inits);
 }
 
 // Flattened alternative to k_rewalk_sorted over the same list
@@ -1249,7 +1241,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
 template <int MODEL, bool DET>
 __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
 {
-    uint32_t steps = 0, accepts = 0;
+    uint32_t steps = 0, accepts = 0, inits = 0;
     const uint64_t cnt = a.counters[2] & kListMask;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t* __restrict__ walks = a.walks;
@@ -1284,7 +1276,7 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
         if (pos < L) {
             uint32_t val = kSent;
             if (w.rc.deg) {
-                val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts);
+                val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
                 steps++;
             }
             walks[(uint64_t)pos * W + li] = val;
@@ -1293,6 +1285,7 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
     }
     wave_add(a.counters + 0, steps);
     wave_add(a.counters + 1, accepts);
+    wave_add(a.counters + 7, inits);
 }
 
 // node2vec MH re-walk by passes (sparse walks: configs[4]'s 1/8 shard, where
@@ -1322,7 +1315,7 @@ __global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* 
                                                      const unsigned long long* __restrict__ in_cnt,
                                                      ParkRec* __restrict__ out, unsigned long long* __restrict__ out_cnt)
 {
-    uint32_t steps = 0, accepts = 0;
+    uint32_t steps = 0, accepts = 0, inits = 0;
     const uint64_t cnt = FRESH ? (a.counters[2] & kListMask) : *in_cnt;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t* __restrict__ walks = a.walks;
@@ -1369,7 +1362,7 @@ __global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* 
         if (has) {
             uint32_t val = kSent;
             const bool live = w.rc.deg != 0;   // a walk at a vertex without out-edges ends
-            if (live) val = walk_step<MODEL, false, PARK>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, &park);
+            if (live) val = walk_step<MODEL, false, PARK>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, inits, &park);
             if (!park) {
                 steps += live;
                 walks[(uint64_t)pos * W + li] = val;
@@ -1392,6 +1385,7 @@ __global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* 
     }
     wave_add(a.counters + 0, steps);
     wave_add(a.counters + 1, accepts);
+    wave_add(a.counters + 7, inits);
 }
 
 // The anchors of the parked states, one per lane over full waves.
@@ -1399,13 +1393,15 @@ __global__ __launch_bounds__(256) void k_park_init(WalkArgs a, ParkRec* in, cons
 {
     const uint64_t cnt = *in_cnt;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t inits = 0;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < cnt; t += stride) {
         const ParkRec pr = in[t];
         const Row rc = load_rec(a.vrec, pr.cur), rp = load_rec(a.vrec, pr.prev);
         uint32_t an = 0, cls = 0;
-        anchor_compute(a, true, rc, rp, an, cls);
+        anchor_compute(a, true, rc, rp, an, cls, inits);
         *(pr.ac ? pr.ac : &in[t].own) = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     }
+    wave_add(a.counters + 7, inits);
 }
 
 void launch_rewalk_park(const WalkArgs& a, int fresh, int park, const void* in, const unsigned long long* in_cnt,

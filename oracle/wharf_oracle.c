@@ -364,12 +364,19 @@ wo_engine* wo_create(uint64_t n, uint64_t m, const uint64_t* off, const uint32_t
     e->adj = (uint32_t*)malloc((m ? m : 1) * 4);
     if (m) memcpy(e->adj, adj, m * 4);
     e->anchor = (uint64_t*)malloc((m ? m : 1) * 8);
-    memset(e->anchor, 0xFF, (m ? m : 1) * 8);
+    /* anchors are read by node2vec MH only: the other modes leave the pages untouched */
+    if (model == WO_NODE2VEC && !deterministic) memset(e->anchor, 0xFF, (m ? m : 1) * 8);
     e->row_epoch = (uint32_t*)calloc(n ? n : 1, 4);
     e->wpv = wpv; e->L = L; e->model = model; e->init = init; e->det = deterministic;
     e->p = p; e->q = q; e->seed = seed;
     e->walks = (uint32_t*)malloc(n * wpv * L * 4 + 4);
-    for (uint64_t i = 0; i < n * wpv * L; i++) e->walks[i] = WO_SENT;
+    /* Corpora above 8 GiB (the full-size GPU tests' windows of configs[3]: 107 GB)
+     * are not pre-filled: generation writes every position of each walk it
+     * produces (walk_from), so wo_time_generate_range + wo_get_walks_range of that
+     * range need no fill, and untouched pages cost no host memory.  Only those two
+     * calls are used on such engines. */
+    if ((uint64_t)n * wpv * L * 4 <= (8ull << 30))
+        for (uint64_t i = 0; i < n * wpv * L; i++) e->walks[i] = WO_SENT;
     return e;
 }
 

@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round-3 GPU session steps (each with its own time limit; a crash/abort/timeout ends the session):
+#   pytest smoke bench prof pmc c4w10 c4w1 c3shard8 ...
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/r3
+export TMPDIR=/tmp
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/r3/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 4 "gpurun_out/r3/$name.log" | cut -c1-400
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    pytest) step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -rf --timeout 300 --timeout-method thread ;;
+    smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  step bench 900 python bench.py ;;
+    prof)   step prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3/prof_bench -o run -- python3 bench.py --cpu-baseline off ;;
+    pmc)    GEN="python3 bench.py --steps 2 --warmup 0 --rewalk-batches 0 --det-rewalk-batches 0 --n2v-steps 2 --n2v-rewalk-batches 0 --cpu-baseline off --per-gpu-of-8 0 --gather-probes 0"
+            STR="python3 bench.py --steps 1 --warmup 0 --rewalk-batches 0 --det-rewalk-batches 3 --n2v-steps 0 --n2v-rewalk-batches 0 --cpu-baseline off --per-gpu-of-8 0 --gather-probes 0"
+            step pmc_gen_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_walk" --output-format csv -d gpurun_out/r3/pmc_gen_fetch -o run -- $GEN
+            step pmc_gen_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_walk" --output-format csv -d gpurun_out/r3/pmc_gen_write -o run -- $GEN
+            step pmc_str_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_rewalk_chunked|k_patch_in_edges" --output-format csv -d gpurun_out/r3/pmc_str_fetch -o run -- $STR
+            step pmc_str_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_rewalk_chunked|k_patch_in_edges" --output-format csv -d gpurun_out/r3/pmc_str_write -o run -- $STR ;;
+    c4w10)  step c4_n2v_wpv10_shard8 600 python tools/bigscale.py --model node2vec --wpv 10 --batches 3 --mixed --no-oracle --shard 8 ;;
+    c4w1)   step c4_n2v_wpv1_shard8 600 python tools/bigscale.py --model node2vec --wpv 1 --batches 3 --mixed --no-oracle --shard 8 ;;
+    c3shard8) step c3_shard8 900 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 5 --shard 8 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
