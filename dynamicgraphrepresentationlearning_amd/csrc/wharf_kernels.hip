@@ -875,6 +875,7 @@ struct ChunkTest {
     uint32_t w[kScanChunk];
 };
 
+template <bool BIG = false>
 __device__ __forceinline__ void chunk_issue(const WalkArgs& a, const uint32_t* s_bloom, const uint32_t (&x)[kScanChunk],
                                             uint32_t cnt, ChunkTest& t)
 {
@@ -882,7 +883,7 @@ __device__ __forceinline__ void chunk_issue(const WalkArgs& a, const uint32_t* s
     t.end = cnt;
 #pragma unroll
     for (uint32_t j = 0; j < kScanChunk; j++) {
-        t.mask |= (uint32_t)bloom_test(s_bloom, x[j]) << j;
+        t.mask |= (uint32_t)(BIG ? bloom_test_big(s_bloom, x[j]) : bloom_test(s_bloom, x[j])) << j;
         if (x[j] == kSent && j < t.end) t.end = j;
     }
     if (t.end < 32) t.mask &= (1u << t.end) - 1u;
@@ -1048,6 +1049,63 @@ __global__ __launch_bounds__(256, COPY ? 1 : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCA
         a.aff[li] = (uint8_t)p;
     }
     if (COPY) wave_add(a.counters + 0, steps);
+}
+
+// The rewalk-point scan alone with the 64-KiB Bloom filter of the in-edge scan
+// (kBigBloomWords, ~0.02 % false positives at 10 k sources instead of ~3 %):
+// with the 16-KiB filter, ~40 % of the 16-position chunks of a walk that does
+// not meet a source carry a false positive whose exact bitmap word costs the
+// wave a round trip — ~1 ms of the 3 ms configs[2] scan
+// (profiles/r02/chunked_scan).  64 KiB of LDS per workgroup: 1024-thread
+// workgroups, two per CU, 8 waves per SIMD as before.
+template <bool NTL>
+__global__ __launch_bounds__(1024, 8) void k_rewalk_scan_big(WalkArgs a)
+{
+    constexpr uint32_t C = kScanChunk;
+    __shared__ uint32_t s_bloom[kBigBloomWords];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    for (uint32_t i = threadIdx.x; i < kBigBloomWords / 4; i += blockDim.x)
+        reinterpret_cast<u32x4*>(s_bloom)[i] = reinterpret_cast<const u32x4*>(a.bloom + kBloomWords)[i];
+    __syncthreads();
+    const uint64_t W = a.W;
+    const uint32_t L = a.L;
+    const XcdRange xr = xcd_range(W);
+    const uint32_t lane = __lane_id();
+    for (uint64_t li = xr.first; li < xr.end; li += xr.stride) {
+        uint32_t p = kNoRewalk;
+        bool scanning = true;
+        const uint32_t* __restrict__ wb = a.walks + uniform64(li - lane);
+        uint32_t cur[C], nxt[C];
+#pragma unroll
+        for (uint32_t j = 0; j < C; j++) cur[j] = j < L ? row_load<NTL>(wb + (uint64_t)j * W, lane) : kSent;
+        for (uint32_t c0 = 0; c0 < L; c0 += C) {
+            const uint32_t cnt = min(C, L - c0);
+            const bool more = c0 + C < L, was_scanning = scanning;
+            ChunkTest ct;
+            if (scanning) chunk_issue<true>(a, s_bloom, cur, cnt, ct);
+            if (more && scanning) {
+#pragma unroll
+                for (uint32_t j = 0; j < C; j++)
+                    nxt[j] = c0 + C + j < L ? row_load<NTL>(wb + (uint64_t)(c0 + C + j) * W, lane) : kSent;
+            }
+            if (scanning) {
+                bool ended = false;
+                const uint32_t j = chunk_resolve(a, cur, cnt, ct, ended);
+                if (j < C) {
+                    p = c0 + j;
+                    scanning = false;
+                } else if (ended) {
+                    scanning = false;
+                }
+            }
+            if (!__any(scanning)) break;
+            if (more && was_scanning) {
+#pragma unroll
+                for (uint32_t j = 0; j < C; j++) cur[j] = nxt[j];
+            }
+        }
+        a.aff[li] = (uint8_t)p;
+    }
 }
 
 __global__ void k_src_index(const RunInfo* __restrict__ runs, uint64_t k, uint32_t* __restrict__ src_idx)
@@ -1491,6 +1549,15 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
         return;
     }
     if (rewalk && a.scan_only && chunked) {
+        // WHARF_SCAN_SMALL_BLOOM=1 (A/B): the 16-KiB filter in 256-thread workgroups
+        const char* sb = getenv("WHARF_SCAN_SMALL_BLOOM");
+        if (!(sb && atoi(sb))) {
+            const dim3 bgrid((std::max<unsigned>(std::min<uint64_t>((a.W + 1023) / 1024, (uint64_t)cu_count() * 2), kXcds) /
+                              kXcds) * kXcds);
+            if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_scan_big<true>), bgrid, dim3(1024), 0, s, a);
+            else hipLaunchKernelGGL((k_rewalk_scan_big<false>), bgrid, dim3(1024), 0, s, a);
+            return;
+        }
         if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<false, true>), mgrid, block, 0, s, a);
         else hipLaunchKernelGGL((k_rewalk_chunked<false, false>), mgrid, block, 0, s, a);
         return;

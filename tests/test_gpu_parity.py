@@ -398,6 +398,8 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     n2v_list, no_slack, no_headroom, filt, no_memo, no_chunked, stab, no_pre, nt_rows = PATHS[path]
     monkeypatch.setenv("WHARF_NT_ROWS", nt_rows)
     monkeypatch.setenv("WHARF_PARK_TAIL", "0" if path == "park/slack" else "8192")
+    # rewalk points alone: the 64-KiB-filter scan (default) or the 16-KiB one in 256-thread workgroups
+    monkeypatch.setenv("WHARF_SCAN_SMALL_BLOOM", "1" if path == "sorted/plain-rows" else "0")
     monkeypatch.setenv("WHARF_NO_PREINIT", no_pre)
     monkeypatch.setenv("WHARF_NO_START_TABLE", "1" if stab == "off" else "0")
     monkeypatch.setenv("WHARF_START_TABLE_BUCKETS", "2" if stab == "tiny" else "0")
