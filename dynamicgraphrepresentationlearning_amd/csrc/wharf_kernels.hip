@@ -875,7 +875,36 @@ struct ChunkTest {
     uint32_t w[kScanChunk];
 };
 
-template <bool BIG = false>
+// FB: the filter in LDS has 4096 << FB words (FB 0: the 16-KiB filter, 1: 32 KiB
+// folded from the 64-KiB one, 2: the 64-KiB one); a key's word is hash >> (20 - FB)
+template <int FB>
+__device__ __forceinline__ bool bloom_test_fb(const uint32_t* f, uint32_t x)
+{
+    const uint32_t h = bloom_mix(x), b = bloom_bits(h);
+    return (f[h >> (20 - FB)] & b) == b;
+}
+static_assert(kBigBloomWords == (kBloomWords << 2), "the big filter is the 16-KiB one at 4x the words");
+
+// the filter of 4096 << FB words into LDS (FB 1: word i = big[2i] | big[2i + 1],
+// a superset filter: keys of either big word share its bit positions)
+template <int FB>
+__device__ __forceinline__ void filter_to_lds(const WalkArgs& a, uint32_t* s_bloom)
+{
+    if constexpr (FB == 0) {
+        for (uint32_t i = threadIdx.x; i < kBloomWords; i += blockDim.x) s_bloom[i] = a.bloom[i];
+    } else if constexpr (FB == 1) {
+        const uint2* big = reinterpret_cast<const uint2*>(a.bloom + kBloomWords);
+        for (uint32_t i = threadIdx.x; i < 2 * kBloomWords; i += blockDim.x) {
+            const uint2 w = big[i];
+            s_bloom[i] = w.x | w.y;
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < kBigBloomWords; i += blockDim.x) s_bloom[i] = a.bloom[kBloomWords + i];
+    }
+    __syncthreads();
+}
+
+template <int FB = 0>
 __device__ __forceinline__ void chunk_issue(const WalkArgs& a, const uint32_t* s_bloom, const uint32_t (&x)[kScanChunk],
                                             uint32_t cnt, ChunkTest& t)
 {
@@ -883,7 +912,7 @@ __device__ __forceinline__ void chunk_issue(const WalkArgs& a, const uint32_t* s
     t.end = cnt;
 #pragma unroll
     for (uint32_t j = 0; j < kScanChunk; j++) {
-        t.mask |= (uint32_t)(BIG ? bloom_test_big(s_bloom, x[j]) : bloom_test(s_bloom, x[j])) << j;
+        t.mask |= (uint32_t)bloom_test_fb<FB>(s_bloom, x[j]) << j;
         if (x[j] == kSent && j < t.end) t.end = j;
     }
     if (t.end < 32) t.mask &= (1u << t.end) - 1u;
@@ -953,12 +982,12 @@ __device__ __forceinline__ XcdRange xcd_range(uint64_t W)
 #ifndef WHARF_SCAN_ONLY_WAVES_EU
 #define WHARF_SCAN_ONLY_WAVES_EU 8
 #endif
-template <bool COPY, bool NTL>
+template <bool COPY, bool NTL, int FB = 0>
 __global__ __launch_bounds__(256, COPY ? 1 : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArgs a)
 {
     constexpr uint32_t C = kScanChunk;
-    __shared__ uint32_t s_bloom[kBloomWords];
-    bloom_to_lds(a, s_bloom);
+    __shared__ uint32_t s_bloom[kBloomWords << FB];
+    filter_to_lds<FB>(a, s_bloom);
     uint32_t steps = 0;
     uint32_t* __restrict__ walks = a.walks;
     const uint64_t W = a.W;
@@ -981,7 +1010,7 @@ __global__ __launch_bounds__(256, COPY ? 1 : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCA
             const bool was_scanning = scanning;
             const bool more = c0 + C < L;
             ChunkTest ct;
-            if (scanning) chunk_issue(a, s_bloom, cur, cnt, ct);
+            if (scanning) chunk_issue<FB>(a, s_bloom, cur, cnt, ct);
             if (!COPY && more && scanning) {
                 // scan only: the next chunk's rows go out before the bitmap words
                 // are waited for (loads complete in order: the wait leaves them in flight)
@@ -1063,10 +1092,7 @@ __global__ __launch_bounds__(1024, 8) void k_rewalk_scan_big(WalkArgs a)
 {
     constexpr uint32_t C = kScanChunk;
     __shared__ uint32_t s_bloom[kBigBloomWords];
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    for (uint32_t i = threadIdx.x; i < kBigBloomWords / 4; i += blockDim.x)
-        reinterpret_cast<u32x4*>(s_bloom)[i] = reinterpret_cast<const u32x4*>(a.bloom + kBloomWords)[i];
-    __syncthreads();
+    filter_to_lds<2>(a, s_bloom);
     const uint64_t W = a.W;
     const uint32_t L = a.L;
     const XcdRange xr = xcd_range(W);
@@ -1082,7 +1108,7 @@ __global__ __launch_bounds__(1024, 8) void k_rewalk_scan_big(WalkArgs a)
             const uint32_t cnt = min(C, L - c0);
             const bool more = c0 + C < L, was_scanning = scanning;
             ChunkTest ct;
-            if (scanning) chunk_issue<true>(a, s_bloom, cur, cnt, ct);
+            if (scanning) chunk_issue<2>(a, s_bloom, cur, cnt, ct);
             if (more && scanning) {
 #pragma unroll
                 for (uint32_t j = 0; j < C; j++)
@@ -1544,8 +1570,16 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
     const bool chunked = !(nc && atoi(nc));
     if (rewalk && a.det && a.memo && !a.scan_only) {
         hipLaunchKernelGGL(k_det_suffix, grid_for((uint64_t)a.wpv * a.memo_k, 256), 256, 0, s, a);
-        if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<true, true>), mgrid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_rewalk_chunked<true, false>), mgrid, block, 0, s, a);
+        // the 32-KiB filter (5 workgroups of 256 per CU still fit the 160 KiB of LDS);
+        // WHARF_COPY_SMALL_BLOOM=1 (A/B): the 16-KiB one
+        const char* cb = getenv("WHARF_COPY_SMALL_BLOOM");
+        if (cb && atoi(cb)) {
+            if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<true, true, 0>), mgrid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_rewalk_chunked<true, false, 0>), mgrid, block, 0, s, a);
+        } else {
+            if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<true, true, 1>), mgrid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_rewalk_chunked<true, false, 1>), mgrid, block, 0, s, a);
+        }
         return;
     }
     if (rewalk && a.scan_only && chunked) {

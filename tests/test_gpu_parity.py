@@ -400,6 +400,8 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     monkeypatch.setenv("WHARF_PARK_TAIL", "0" if path == "park/slack" else "8192")
     # rewalk points alone: the 64-KiB-filter scan (default) or the 16-KiB one in 256-thread workgroups
     monkeypatch.setenv("WHARF_SCAN_SMALL_BLOOM", "1" if path == "sorted/plain-rows" else "0")
+    # deterministic suffix copy: the 32-KiB filter folded from the 64-KiB one (default) or the 16-KiB one
+    monkeypatch.setenv("WHARF_COPY_SMALL_BLOOM", "1" if path == "sorted/plain-rows" else "0")
     monkeypatch.setenv("WHARF_NO_PREINIT", no_pre)
     monkeypatch.setenv("WHARF_NO_START_TABLE", "1" if stab == "off" else "0")
     monkeypatch.setenv("WHARF_START_TABLE_BUCKETS", "2" if stab == "tiny" else "0")
