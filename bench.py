@@ -130,7 +130,7 @@ def gather_ceiling(steps_per_s: float, live):
             "source": "tools/gather_roof 3.48 coarse dep, this box, before the timed region"}
 
 
-PMC_ROUNDS = ("r02_", "")   # newest round's rocprofv3 summary first
+PMC_ROUNDS = ("r03_", "r02_", "")   # newest round's rocprofv3 summary first
 
 
 def load_traffic(tag: str):
@@ -426,8 +426,12 @@ def streaming_rooflines(rewalk, rewalk_det, scale):
     in-edge record scan of the slack-row CSR update 4 B per pool slot (the
     slots' targets are read; the few records of sources' in-edges written)."""
     out = {}
-    pmc_rel = os.path.join("profiles", f"pmc_r02_streaming_s{scale}.json")
-    pmc = json.load(open(os.path.join(REPO, pmc_rel))) if os.path.exists(os.path.join(REPO, pmc_rel)) else {}
+    pmc, pmc_rel = {}, None
+    for pre in PMC_ROUNDS:   # the newest round's PMC pass of the same stream
+        rel = os.path.join("profiles", f"pmc_{pre}streaming_s{scale}.json")
+        if os.path.exists(os.path.join(REPO, rel)):
+            pmc, pmc_rel = json.load(open(os.path.join(REPO, rel))), rel
+            break
 
     def ent(name, kernel, bytes_, ms, per):
         if not ms:
@@ -443,9 +447,9 @@ def streaming_rooflines(rewalk, rewalk_det, scale):
         return e
     if rewalk_det:
         pos = rewalk_det["stored_positions_rank0"]
-        out["rewalk_point_scan"] = ent("rewalk_point_scan", "k_rewalk_chunked<false> (apply_walk_updates=false)",
+        out["rewalk_point_scan"] = ent("rewalk_point_scan", "k_rewalk_scan_big (apply_walk_updates=false)",
                                        4 * pos, rewalk_det.get("scan_only_median_ms"), "4 B per stored position")
-        out["deterministic_rewalk_copy"] = ent("deterministic_rewalk_copy", "k_det_suffix + k_rewalk_chunked<true>",
+        out["deterministic_rewalk_copy"] = ent("deterministic_rewalk_copy", "k_det_suffix + k_rewalk_chunked<true, NTL, 1>",
                                                4 * pos, rewalk_det["median_rewalk_kernel_ms"],
                                                "4 B per stored position")
     src = rewalk or rewalk_det
