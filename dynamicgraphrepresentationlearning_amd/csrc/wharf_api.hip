@@ -105,6 +105,7 @@ struct wharf_handle {
     DevBuf preoff;                             // node2vec MH: per-source degree prefix of the anchor pre-init
     DevBuf stab;                               // node2vec MH re-walk: start-state anchor table (k_rewalk_sorted)
     DevBuf park, parkc;                        // node2vec MH re-walk passes: two parked-walker lists, their counts
+    DevBuf bdesc;                              // node2vec MH block re-walk: per 256-walk block, its run of the list
     uint32_t st_park_passes = 0;               // passes of the last re-walk by passes (0: lock-step kernel)
     uint64_t start_bound = 0;                  // distinct re-walk start states of the next walk update, at most (0: unknown)
     wharf_stats st{};
@@ -645,7 +646,7 @@ void free_handle(wharf_handle* h)
                       &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->walks, &h->aff, &h->rtab,
                       &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags, &h->chg, &h->cf,
                       &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel, &h->defer, &h->rplan, &h->pscan,
-                      &h->scratch, &h->stab, &h->preoff, &h->park, &h->parkc})
+                      &h->scratch, &h->stab, &h->preoff, &h->park, &h->parkc, &h->bdesc})
         b->release();
     h->free_snaps();
     for (auto& e : h->ev)
@@ -761,6 +762,11 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         if (a.model == kNode2Vec && !a.det) {   // k_rewalk_plan's compacted, sorted re-walk list
             h->defer.ensure(h->W * 8);
             a.defer = h->defer.as<uint64_t>();
+            const char* rwm = getenv("WHARF_N2V_REWALK");   // =block: k_rewalk_block (row-staged stores)
+            if (rwm && std::string(rwm) == "block" && !a.scan_only) {
+                h->bdesc.ensure(((h->W + 255) / 256) * 8);
+                a.bdesc = h->bdesc.as<uint64_t>();
+            }
             const char* no_stab = getenv("WHARF_NO_START_TABLE");   // A/B and tests: binary search at every start
             if (!a.scan_only && k && !(no_stab && atoi(no_stab))) {
                 // start states (x, prev): x a batch source, prev an in-neighbour of it, so at most
@@ -1244,6 +1250,7 @@ int wharf_set_shard(wharf_handle* h, uint64_t lo, uint64_t hi)
         h->aff.release();
         h->defer.release();
         h->park.release();
+        h->bdesc.release();
         h->lo = lo;
         h->hi = hi;
         h->n_loc = hi - lo;

@@ -43,6 +43,7 @@ struct WalkArgs {
     int model, init, det;
     int scan_only;               // re-walk: only find rewalk points (apply_walk_updates=false)
     uint64_t* defer;             // node2vec re-walk list {li | p << 56}, tickets << 40 | count in counters[2]
+    uint64_t* bdesc;             //   per 256-walk block: its run of the list {offset | count << 40}, or null
     uint64_t* stab;              // node2vec MH re-walk: start-state table, buckets of 4 {key, anchor entry}, or null
     uint64_t stab_mask;          //   buckets - 1
     // deterministic re-walk by suffix table (k_det_suffix + k_rewalk_chunked<true>), or memo == null

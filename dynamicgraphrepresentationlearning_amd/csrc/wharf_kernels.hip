@@ -1250,6 +1250,7 @@ __global__ __launch_bounds__(256) WHARF_SCAN_WAVES void k_rewalk_plan(WalkArgs a
         const uint32_t nact = s_bin[255];                  // entries ranked before the "none" bin
         if (t == 0) s_ticket = nact ? atomicAdd(a.counters + 2, (1ull << 40) | nact) : 0ull;
         __syncthreads();
+        if (t == 0 && a.bdesc) a.bdesc[base >> 8] = (s_ticket & kListMask) | ((uint64_t)nact << 40);
         if (key != 255u) {
             const uint32_t rank = atomicAdd(&s_bin[key], 1u);
             const uint64_t tk = s_ticket;
@@ -1309,6 +1310,88 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
             // matrix rows whole cost as much (sorted 57 -> 47 ms, merge 9.8 ms;
             // profiles/r02/n2v_rewalk2)
             if (active && pos > p) __builtin_nontemporal_store(val, walks + (uint64_t)pos * W + li);
+        }
+    }
+    wave_add(a.counters + 0, steps);
+    wave_add(a.counters + 1, accepts);
+    wave_add(a.counters + 7, inits);
+}
+
+// Block-staged alternative to k_rewalk_sorted (WHARF_N2V_REWALK=block): a
+// workgroup takes one 256-walk block's run of the list (k_rewalk_plan's
+// bdesc), wave w its entries [64 w, 64 w + 64), and sweeps positions in chunks
+// of kTileRows; the new values go to an LDS tile [kTileRows][256] and each
+// position of the chunk leaves as ONE full 1-KiB row segment of the walk
+// matrix — the columns that are not re-walked there (walks of the block that do
+// not re-walk, or are still before their rewalk point) read their old value back
+// (a coalesced row read).  k_rewalk_sorted's lanes are walks scattered over a
+// block, so its stores are partial lines (446 M write requests for 5.3 GB of
+// values per configs[2] batch; a timing probe without them ran 43 vs 55 ms).
+constexpr uint32_t kTileRows = 16;
+
+template <int MODEL>
+__global__ __launch_bounds__(256) void k_rewalk_block(WalkArgs a)
+{
+    __shared__ uint32_t tile[kTileRows][256];
+    __shared__ uint32_t pcol[256];   // rewalk point of each column of the block, or kNoRewalk
+    __shared__ uint32_t s_first;
+    if (blockDim.x != 256) __builtin_trap();   // one column per thread
+    uint32_t steps = 0, accepts = 0, inits = 0;
+    uint32_t* __restrict__ walks = a.walks;
+    const uint64_t W = a.W, nblk = (W + 255) >> 8;
+    const uint32_t L = a.L, ep = a.epoch << 4, t = threadIdx.x;
+    for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const uint64_t d = a.bdesc[b];
+        const uint32_t cnt = (uint32_t)(d >> 40);
+        if (cnt == 0) continue;   // (uniform over the workgroup)
+        const uint64_t base = b << 8;
+        pcol[t] = kNoRewalk;
+        if (t == 0) s_first = L;
+        __syncthreads();
+        const bool active = t < cnt;
+        uint64_t li = 0;
+        uint32_t p = L, wlo = 0, whi = 0;
+        Walker w;
+        w.rc.deg = 0;
+        if (active) {
+            const uint64_t ent = a.defer[(d & kListMask) + t];
+            li = ent & ((1ull << 56) - 1);
+            p = (uint32_t)(ent >> 56);
+            const uint64_t r = li / a.n_loc;
+            const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
+            wlo = (uint32_t)wid;
+            whi = (uint32_t)(wid >> 32);
+            pcol[li - base] = p;
+            atomicMin(&s_first, p + 1);
+            const uint32_t x = walks[(uint64_t)p * W + li];
+            const uint32_t xprev = p ? walks[(uint64_t)(p - 1) * W + li] : x;
+            walk_state<MODEL, false>(a, x, xprev, p, wlo, whi, ep, w);
+        }
+        __syncthreads();
+        const uint32_t first = s_first, pc = pcol[t];
+        const uint64_t col = base + t;
+        for (uint32_t c0 = first; c0 < L; c0 += kTileRows) {
+            const uint32_t rows = min(kTileRows, L - c0);
+            for (uint32_t j = 0; j < rows; j++) {
+                const uint32_t pos = c0 + j;
+                if (active && pos > p) {
+                    uint32_t val = kSent;
+                    if (w.rc.deg) {
+                        val = walk_step<MODEL, false>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, inits);
+                        steps++;
+                    }
+                    tile[j][li - base] = val;
+                }
+            }
+            __syncthreads();
+            if (col < W) {
+                for (uint32_t j = 0; j < rows; j++) {
+                    const uint64_t at = (uint64_t)(c0 + j) * W + col;
+                    const uint32_t v = (pc != kNoRewalk && c0 + j > pc) ? tile[j][t] : walks[at];
+                    __builtin_nontemporal_store(v, walks + at);
+                }
+            }
+            __syncthreads();
         }
     }
     wave_add(a.counters + 0, steps);
@@ -1555,7 +1638,8 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
         if (rewalk && M == kNode2Vec) {                                                      \
             hipLaunchKernelGGL(k_rewalk_plan, grid, block, 0, s, a);                         \
             if (!a.scan_only && !a.park) { /* park: the host runs the passes */              \
-                if (flat_list()) hipLaunchKernelGGL((k_rewalk_list<M, D>), lgrid, block, 0, s, a); \
+                if (a.bdesc) hipLaunchKernelGGL((k_rewalk_block<M>), lgrid, block, 0, s, a);     \
+                else if (flat_list()) hipLaunchKernelGGL((k_rewalk_list<M, D>), lgrid, block, 0, s, a); \
                 else hipLaunchKernelGGL((k_rewalk_sorted<M, D>), lgrid, block, 0, s, a);     \
             }                                                                                \
         } else if (rewalk) {                                                                 \

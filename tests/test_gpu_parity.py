@@ -362,6 +362,9 @@ def test_affected_ids_on_device_match_host_list(W):
 # left (WHARF_PARK_TAIL=0) or finishing a short list with in-wave inits (the default tail)
 PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0", "on", "0", "1"),
          "park/slack": ("park", "0", "0", "on", "1", "0", "on", "1", "1"),
+         "sorted/move-lazy": ("sorted", "1", "0", "on", "1", "0", "on", "1", "0"),
+         "block/slack": ("block", "0", "0", "on", "0", "0", "on", "0", "1"),
+         "block/move-lazy": ("block", "1", "0", "noslack", "1", "0", "tiny", "1", "0"),
          "park/repack-tail": ("park", "1", "1", "off", "0", "1", "tiny", "0", "0"),
          "flat/move": ("flat", "1", "0", "noslack", "0", "0", "off", "0", "0"),
          "sorted/repack": ("sorted", "1", "1", "off", "0", "1", "tiny", "0", "1"),
