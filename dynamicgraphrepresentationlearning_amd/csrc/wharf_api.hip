@@ -10,6 +10,7 @@
 #include <rocprim/device/device_select.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
+#include <charconv>
 #include <chrono>
 #include <stdexcept>
 #include <string>
@@ -1281,6 +1282,13 @@ int wharf_get_graph(wharf_handle* h, uint64_t* offsets_out, uint32_t* targets_ou
     });
 }
 
+// WHARF_WALK_NO_SNAPSHOT=1 (A/B, tools/walk_readout): walk() / vertex_at_walk() read the device per call
+static bool no_snapshot()
+{
+    const char* e = getenv("WHARF_WALK_NO_SNAPSHOT");
+    return e && atoi(e);
+}
+
 static uint64_t local_index(wharf_handle* h, uint64_t wid)
 {
     const uint64_t r = wid / h->n, v = wid % h->n;
@@ -1295,7 +1303,14 @@ int wharf_walk(wharf_handle* h, uint64_t wid, uint32_t* out, uint32_t* len)
         REQUIRE(h && out && len, WHARF_E_INVALID, "null argument");
         const uint64_t li = local_index(h, wid);
         h->ensure_walks();
-        std::memcpy(out, h->snap_row(li), h->L * 4);
+        if (no_snapshot()) {   // A/B: one gather kernel, D2H and sync per call (round 2's path)
+            h->sel.ensure(h->L * 4);
+            launch_gather_rows(h->walks.as<uint32_t>(), h->W, h->L, nullptr, li, 1, h->sel.as<uint32_t>(), h->s);
+            HIPCHK(hipMemcpyAsync(out, h->sel.p, h->L * 4, hipMemcpyDeviceToHost, h->s));
+            h->sync();
+        } else {
+            std::memcpy(out, h->snap_row(li), h->L * 4);
+        }
         uint32_t c = 0;
         while (c < h->L && out[c] != kSent) c++;
         *len = c;
@@ -1304,19 +1319,25 @@ int wharf_walk(wharf_handle* h, uint64_t wid, uint32_t* out, uint32_t* len)
 
 int wharf_walk_string(wharf_handle* h, uint64_t wid, char* buf, size_t cap, size_t* len)
 {
-    std::vector<uint32_t> v(h ? h->L : 1);
+    uint32_t v[256];   // walk_length <= 255 (types::Position is u8)
     uint32_t cnt = 0;
-    int rc = wharf_walk(h, wid, v.data(), &cnt);
+    int rc = wharf_walk(h, wid, v, &cnt);
     if (rc) return rc;
-    std::string s;
-    for (uint32_t i = 0; i < cnt; i++) { s += std::to_string(v[i]); s += ' '; }   // wharfmh.h:375
-    if (len) *len = s.size();
+    char s[256 * 11 + 1];   // "v0 v1 ... " (wharfmh.h:375): <= 10 digits and a space per vertex
+    char* e = s;
+    for (uint32_t i = 0; i < cnt; i++) {
+        e = std::to_chars(e, s + sizeof(s), v[i]).ptr;
+        *e++ = ' ';
+    }
+    *e = 0;
+    const size_t n = (size_t)(e - s);
+    if (len) *len = n;
     if (buf) {
-        if (cap < s.size() + 1) {
+        if (cap < n + 1) {
             set_err(h, "buffer too small");
             return WHARF_E_INVALID;
         }
-        std::memcpy(buf, s.c_str(), s.size() + 1);
+        std::memcpy(buf, s, n + 1);
     }
     return WHARF_OK;
 }
@@ -1328,7 +1349,13 @@ int wharf_vertex_at_walk(wharf_handle* h, uint64_t wid, uint32_t position, uint3
         REQUIRE(position < h->L, WHARF_E_RANGE, "position >= walk_length");
         const uint64_t li = local_index(h, wid);
         h->ensure_walks();
-        *vertex = h->snap_row(li)[position];
+        if (no_snapshot()) {
+            HIPCHK(hipMemcpyAsync(vertex, h->walks.as<uint32_t>() + (uint64_t)position * h->W + li, 4,
+                                  hipMemcpyDeviceToHost, h->s));
+            h->sync();
+        } else {
+            *vertex = h->snap_row(li)[position];
+        }
     });
 }
 

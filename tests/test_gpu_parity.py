@@ -525,6 +525,52 @@ def test_pool_exhausted_leaves_the_handle_unchanged(W, monkeypatch):
     g.destroy()
 
 
+def test_walk_readout_snapshot_follows_every_change(W, monkeypatch):
+    """walk() / vertex_at_walk() read a pinned host snapshot of the walk matrix
+    (chunks of 64 Ki walks, taken on first use); every change to the walks —
+    generation, an update with its re-walk, batch_walk_update, destroy_index,
+    set_shard — invalidates it.  After each, every walk read through the
+    snapshot equals the exported corpus and the per-call device path
+    (WHARF_WALK_NO_SNAPSHOT=1), text included."""
+    base = O.generate_batch_of_edges(60000, 1 << 17, 4, False, False)
+    off, adj = O.csr_from_edges(1 << 16, base)          # 2 snapshot chunks per round: several chunks in play
+    cfg = W.WharfConfig(walks_per_vertex=2, walk_length=12, deterministic=False, seed=3)
+    g = W.WharfMH.from_csr(off, adj, config=cfg)
+    rng = np.random.default_rng(5)
+
+    def check():
+        w = g.walks()
+        ids = rng.choice(g.number_of_walks, 300, replace=False)
+        for i in ids:
+            row = w[i][w[i] != W.SENTINEL]
+            assert np.array_equal(g.walk_vertices(int(i)), row)
+            assert g.walk(int(i)) == O.walk_string(w[i])
+            assert g.vertex_at_walk(int(i), 0) == int(w[i][0])
+        monkeypatch.setenv("WHARF_WALK_NO_SNAPSHOT", "1")
+        for i in ids[:50]:
+            assert g.walk(int(i)) == O.walk_string(w[i])
+        monkeypatch.setenv("WHARF_WALK_NO_SNAPSHOT", "0")
+
+    g.generate_initial_random_walks()
+    check()
+    b = O.generate_batch_of_edges(3000, 1 << 16, 9, False, False)
+    g.insert_edges_batch(b, remove_dups=True)
+    check()
+    g.batch_walk_update(b[:100, 0])
+    check()
+    g.delete_edges_batch(b, remove_dups=True)
+    check()
+    g.destroy_index()
+    assert g.walk(5) == O.walk_string(g.walks()[5]) == ""   # no walks left: the snapshot was dropped too
+    g.set_shard(1000, 30000)
+    g.generate_initial_random_walks()
+    w = g.walks()
+    ids = g.walk_ids()
+    for j in (0, 17, len(ids) - 1):
+        assert g.walk(int(ids[j])) == O.walk_string(w[j])
+    g.destroy()
+
+
 # ---------------------------------------------------------------------------
 # MH mode
 # ---------------------------------------------------------------------------

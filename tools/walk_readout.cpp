@@ -1,0 +1,57 @@
+// Corpus readout through the C ABI, the way the reference's own exporter does it:
+// WharfMH::walk(i) once per walk, in order (experiments/src/vertex-classification.cpp:145-148).
+// Times wharf_walk_string over the first `n_old` walks with a device read per call
+// (WHARF_WALK_NO_SNAPSHOT=1, round 2's path) and over the first `n_new` walks through
+// the host snapshot, on configs[1]'s graph (RMAT scale 22, 117 M samples, wpv 10, L 80).
+//
+//   tools/walk_readout [n_old=20000] [n_new=41943040]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "wharf_gpu.h"
+
+static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+int main(int argc, char** argv)
+{
+    const uint64_t n_old = argc > 1 ? strtoull(argv[1], nullptr, 10) : 20000;
+    uint64_t n_new = argc > 2 ? strtoull(argv[2], nullptr, 10) : 41943040;
+    wharf_config cfg;
+    wharf_config_default(&cfg);
+    cfg.deterministic = 0;
+    wharf_handle* h = nullptr;
+    const uint64_t n = 1ull << 22;
+    if (wharf_create_rmat(&cfg, n, 117185083, 2 * n, 2, 0.5, 0.2, 0.1, 0, &h) || wharf_generate(h)) {
+        fprintf(stderr, "setup failed: %s\n", wharf_last_error(h));
+        return 1;
+    }
+    uint64_t W = 0;
+    wharf_shard(h, nullptr, nullptr, &W);
+    if (n_new > W) n_new = W;
+    std::vector<char> buf(80 * 11 + 1);
+    size_t len = 0, total = 0;
+    setenv("WHARF_WALK_NO_SNAPSHOT", "1", 1);
+    double t0 = now();
+    for (uint64_t i = 0; i < n_old; i++) {
+        if (wharf_walk_string(h, i, buf.data(), buf.size(), &len)) return 2;
+        total += len;
+    }
+    const double t_old = now() - t0;
+    unsetenv("WHARF_WALK_NO_SNAPSHOT");
+    t0 = now();
+    for (uint64_t i = 0; i < n_new; i++) {
+        if (wharf_walk_string(h, i, buf.data(), buf.size(), &len)) return 3;
+        total += len;
+    }
+    const double t_new = now() - t0;
+    printf("{\"walks\": %llu, \"per_call_device_read\": {\"calls\": %llu, \"seconds\": %.3f, \"us_per_call\": %.2f, "
+           "\"all_walks_seconds_extrapolated\": %.1f}, \"host_snapshot\": {\"calls\": %llu, \"seconds\": %.3f, "
+           "\"us_per_call\": %.3f, \"all_walks_seconds\": %.1f}, \"chars\": %zu}\n",
+           (unsigned long long)W, (unsigned long long)n_old, t_old, 1e6 * t_old / n_old, t_old / n_old * W,
+           (unsigned long long)n_new, t_new, 1e6 * t_new / n_new, t_new / n_new * W, total);
+    wharf_destroy(h);
+    return 0;
+}
