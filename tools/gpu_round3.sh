@@ -36,6 +36,7 @@ for s in "$@"; do
     c4w10)  step c4_n2v_wpv10_shard8 600 python tools/bigscale.py --model node2vec --wpv 10 --batches 3 --mixed --no-oracle --shard 8 ;;
     c4w1)   step c4_n2v_wpv1_shard8 600 python tools/bigscale.py --model node2vec --wpv 1 --batches 3 --mixed --no-oracle --shard 8 ;;
     c3shard8) step c3_shard8 900 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 5 --shard 8 ;;
+    readout) step walk_readout 400 tools/walk_readout 20000 41943040 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
