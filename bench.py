@@ -447,7 +447,7 @@ def streaming_rooflines(rewalk, rewalk_det, scale):
         return e
     if rewalk_det:
         pos = rewalk_det["stored_positions_rank0"]
-        out["rewalk_point_scan"] = ent("rewalk_point_scan", "k_rewalk_scan_big (apply_walk_updates=false)",
+        out["rewalk_point_scan"] = ent("rewalk_point_scan", "k_rewalk_scan_lean (apply_walk_updates=false)",
                                        4 * pos, rewalk_det.get("scan_only_median_ms"), "4 B per stored position")
         out["deterministic_rewalk_copy"] = ent("deterministic_rewalk_copy", "k_det_suffix + k_rewalk_chunked<true, NTL, 1>",
                                                4 * pos, rewalk_det["median_rewalk_kernel_ms"],

@@ -735,6 +735,10 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         HIPCHK(hipMemsetAsync(h->counters.p, 0, 24, s));
         HIPCHK(hipMemsetAsync(h->counters.as<unsigned long long>() + 7, 0, 8, s));
         h->st_park_passes = 0;
+        // tests: WHARF_BLOOM_SATURATE=1 sets every bit of the walk kernels' source
+        // filters, so every position is a positive and the exact checks decide
+        const char* sat = getenv("WHARF_BLOOM_SATURATE");
+        if (sat && atoi(sat)) HIPCHK(hipMemsetAsync(h->bitmap.as<uint32_t>() + h->bitmap_words(), 0xFF, kFilterWords * 4, s));
         WalkArgs a = h->walk_args();
         a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
         // chunked scans: non-temporal row loads when most walks are expected to re-walk.  The

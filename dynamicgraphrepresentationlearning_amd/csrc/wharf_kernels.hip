@@ -1134,6 +1134,125 @@ __global__ __launch_bounds__(1024, 8) void k_rewalk_scan_big(WalkArgs a)
     }
 }
 
+// The rewalk-point scan with the fewest instructions per position (round 3).
+// SQ counters of k_rewalk_scan_big on configs[2] (profiles/r03/scan_kernels):
+// 29.5 VALU + 8.6 SALU per walk position, issue stalls 31 % and waitcnt
+// stalls 43 % of wave cycles: the scan is bound by instruction issue as much
+// as by HBM.  Here, per position: the filter hash (3), its LDS word (1), the
+// three bit tests as shifts of the word (7) and the mask bit (2); per chunk:
+// the walk-end test on the last position only (a walk that ends leaves kSent
+// in the rest of its row), the bitmap word of the first positive only, and
+// the 16 row loads from one buffer descriptor per chunk with the row offsets
+// in SGPRs (1 SALU + 1 load per row, no per-row branch), issued after that
+// word's load so the wait for it leaves the rows in flight.  A false
+// positive (~0.1 % of positions with the 64-KiB filter) falls back to the
+// chunk's next positive, re-read from HBM.  Needs 15 * 4 * W < 2^32 (the host
+// uses k_rewalk_scan_big beyond).
+template <bool NTL>
+__device__ __forceinline__ void lean_chunk(const uint32_t* wb, uint32_t r0, uint32_t L, uint64_t W, uint32_t voff,
+                                           uint32_t (&Y)[kScanChunk])
+{
+    // always 16 loads and no branch (the compiler can then count them); rows
+    // past the walk length re-read the last row (only a partial last chunk)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(wb + (uint64_t)r0 * W), 0, 0xFFFFFFFF,
+                                                                        kRowRsrcFlags);
+    const uint32_t w4 = (uint32_t)W * 4u, top = L - 1 - r0;
+#pragma unroll
+    for (uint32_t j = 0; j < kScanChunk; j++)
+        Y[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, (j < top ? j : top) * w4, NTL ? 2 : 0);
+}
+
+template <bool NTL>
+__global__ __launch_bounds__(1024, 8) void k_rewalk_scan_lean(WalkArgs a)
+{
+    constexpr uint32_t C = kScanChunk;
+    __shared__ uint32_t s_bloom[kBigBloomWords];
+    filter_to_lds<2>(a, s_bloom);
+    const uint64_t W = a.W;
+    const uint32_t L = a.L;
+    const XcdRange xr = xcd_range(W);
+    const uint32_t lane = __lane_id();
+    const uint32_t xend = (uint32_t)xr.end, xstride = (uint32_t)xr.stride;
+    for (uint32_t li = (uint32_t)xr.first; li < xend; li += xstride) {
+        const uint32_t* __restrict__ wb = a.walks + __builtin_amdgcn_readfirstlane(li - lane);
+        // one chunk buffer: the chunk is dead once its first positive is picked,
+        // so the next chunk's loads reuse its registers
+        uint32_t X[C];
+        lean_chunk<NTL>(wb, 0, L, W, lane * 4, X);
+        uint32_t p = kNoRewalk;
+        bool scanning = true;
+        uint32_t mask, x0, j0, w0;
+        bool ended;
+        // the filter test of chunk c0 and the bitmap word of its first positive
+        auto test = [&](uint32_t c0) {
+            const uint32_t cnt = min(C, L - c0);
+            mask = 0;
+            ended = false;
+            if (scanning) {
+#pragma unroll
+                for (uint32_t j = 0; j < C; j++) {
+                    const uint32_t h = bloom_mix(X[j]);
+                    const uint32_t fw = s_bloom[h >> 18];
+                    // bloom_bits(h) all set in fw: the three bits tested in place
+                    uint32_t t = (fw >> ((h >> 13) & 31u)) & (fw >> ((h >> 8) & 31u));
+                    if (WHARF_BLOOM_K > 2) t &= fw >> ((h >> 3) & 31u);
+                    mask |= (t & 1u) << j;
+                }
+                if (cnt < C) mask &= (1u << cnt) - 1u;
+                const uint32_t last = cnt == C ? X[C - 1] : chunk_pick(X, cnt - 1);
+                if (last == kSent) {   // the walk ends in this chunk: positives stop at its end
+                    ended = true;
+                    uint32_t e = cnt;
+#pragma unroll
+                    for (int j = (int)C - 1; j >= 0; j--)
+                        if (X[j] == kSent) e = (uint32_t)j;
+                    mask &= (1u << e) - 1u;
+                }
+            }
+            x0 = 0, j0 = 0, w0 = 0;
+            if (mask) {
+                j0 = (uint32_t)__builtin_ctz(mask);
+                x0 = chunk_pick(X, j0);
+                w0 = a.bitmap[x0 >> 5];
+            }
+        };
+        // settle chunk c0 from its first positive's word
+        auto settle = [&](uint32_t c0) {
+            if (mask) {
+                bool hit = (w0 >> (x0 & 31u)) & 1u;
+                while (!hit) {   // a false positive: the next one, re-read from HBM (rare)
+                    mask &= mask - 1u;
+                    if (!mask) break;
+                    j0 = (uint32_t)__builtin_ctz(mask);
+                    x0 = walk_load<false>(wb + (uint64_t)(c0 + j0) * W + lane);
+                    hit = (a.bitmap[x0 >> 5] >> (x0 & 31u)) & 1u;
+                }
+                if (hit) {
+                    p = c0 + j0;
+                    scanning = false;
+                }
+            }
+            if (ended) scanning = false;
+        };
+        uint32_t c0 = 0;
+        bool done = false;
+        for (; c0 + C < L; c0 += C) {   // chunks with a successor: its 16 loads, unconditional
+            test(c0);
+            lean_chunk<NTL>(wb, c0 + C, L, W, lane * 4, X);
+            settle(c0);
+            if (!__any(scanning)) {
+                done = true;
+                break;
+            }
+        }
+        if (!done) {   // the last chunk
+            test(c0);
+            settle(c0);
+        }
+        a.aff[li] = (uint8_t)p;
+    }
+}
+
 __global__ void k_src_index(const RunInfo* __restrict__ runs, uint64_t k, uint32_t* __restrict__ src_idx)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < k; i += (uint64_t)gridDim.x * blockDim.x)
@@ -1603,6 +1722,7 @@ unsigned cu_count()
     return (unsigned)cus;
 }
 
+
 static unsigned walk_grid(uint64_t W)
 {
     static int per_cu = -1;
@@ -1667,11 +1787,20 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
         return;
     }
     if (rewalk && a.scan_only && chunked) {
-        // WHARF_SCAN_SMALL_BLOOM=1 (A/B): the 16-KiB filter in 256-thread workgroups
+        // WHARF_SCAN_KERNEL (A/B and tests): lean (default) = k_rewalk_scan_lean, 64-KiB
+        // filter, where 15 * 4 * W fits 32 bits; big = k_rewalk_scan_big (round 2, also lean's
+        // fallback); WHARF_SCAN_SMALL_BLOOM=1: k_rewalk_chunked<false> with the 16-KiB filter
         const char* sb = getenv("WHARF_SCAN_SMALL_BLOOM");
-        if (!(sb && atoi(sb))) {
-            const dim3 bgrid((std::max<unsigned>(std::min<uint64_t>((a.W + 1023) / 1024, (uint64_t)cu_count() * 2), kXcds) /
-                              kXcds) * kXcds);
+        const char* sk = getenv("WHARF_SCAN_KERNEL");
+        const bool small = sb && atoi(sb), big = sk && std::string(sk) == "big";
+        const dim3 bgrid((std::max<unsigned>(std::min<uint64_t>((a.W + 1023) / 1024, (uint64_t)cu_count() * 2), kXcds) /
+                          kXcds) * kXcds);
+        if (!small && !big && 15ull * 4ull * a.W < (1ull << 32)) {
+            if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_scan_lean<true>), bgrid, dim3(1024), 0, s, a);
+            else hipLaunchKernelGGL((k_rewalk_scan_lean<false>), bgrid, dim3(1024), 0, s, a);
+            return;
+        }
+        if (!small) {
             if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_scan_big<true>), bgrid, dim3(1024), 0, s, a);
             else hipLaunchKernelGGL((k_rewalk_scan_big<false>), bgrid, dim3(1024), 0, s, a);
             return;

@@ -401,8 +401,12 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     n2v_list, no_slack, no_headroom, filt, no_memo, no_chunked, stab, no_pre, nt_rows = PATHS[path]
     monkeypatch.setenv("WHARF_NT_ROWS", nt_rows)
     monkeypatch.setenv("WHARF_PARK_TAIL", "0" if path == "park/slack" else "8192")
-    # rewalk points alone: the 64-KiB-filter scan (default) or the 16-KiB one in 256-thread workgroups
+    # rewalk points alone: k_rewalk_scan_lean (default); k_rewalk_scan_big (round 2), or with the
+    # 16-KiB filter k_rewalk_chunked<false>.  Every filter bit set on two paths (every position a
+    # positive: the exact checks and the lean scan's false-positive fallback decide)
     monkeypatch.setenv("WHARF_SCAN_SMALL_BLOOM", "1" if path == "sorted/plain-rows" else "0")
+    monkeypatch.setenv("WHARF_SCAN_KERNEL", "big" if path in ("flat/move", "block/move-lazy") else "lean")
+    monkeypatch.setenv("WHARF_BLOOM_SATURATE", "1" if path in ("sorted/lazy-inits", "block/slack") else "0")
     # deterministic suffix copy: the 32-KiB filter folded from the 64-KiB one (default) or the 16-KiB one
     monkeypatch.setenv("WHARF_COPY_SMALL_BLOOM", "1" if path == "sorted/plain-rows" else "0")
     monkeypatch.setenv("WHARF_NO_PREINIT", no_pre)

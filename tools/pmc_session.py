@@ -101,7 +101,7 @@ def main():
                 if KEEP.search(r["Kernel_Name"]):
                     wr.writerow(r)
         out[f"{rnd}_streaming_s22"] = {
-            "rewalk_point_scan": summary("k_rewalk_scan_big", pmc["pmc_str_fetch"], pmc["pmc_str_write"], trs),
+            "rewalk_point_scan": summary("k_rewalk_scan_", pmc["pmc_str_fetch"], pmc["pmc_str_write"], trs),
             "deterministic_rewalk_copy": summary("k_rewalk_chunked<true", pmc["pmc_str_fetch"], pmc["pmc_str_write"], trs),
             "in_edge_scan": summary("k_patch_in_edges", pmc["pmc_str_fetch"], pmc["pmc_str_write"], trs),
             "note": "configs[2] deterministic stream (bench.py --det-rewalk-batches 3): PMC passes and the "
