@@ -2361,24 +2361,31 @@ __global__ __launch_bounds__(1024, 8) void k_patch_in_edges(const uint32_t* __re
     for (uint32_t i = threadIdx.x; i < kBigBloomWords / 4; i += blockDim.x)
         reinterpret_cast<u32x4*>(s_bloom)[i] = reinterpret_cast<const u32x4*>(bloom_big)[i];
     __syncthreads();
-    const uint64_t n4 = slots / 4, stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // 32-bit 16-B-group indices (a pool of < 2^34 slots); the Bloom test as shifts of the
+    // filter word (the lean scan's form: ~11 VALU per slot instead of ~15)
+    const uint32_t n4 = (uint32_t)(slots / 4), stride = gridDim.x * blockDim.x;
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const u32x4* __restrict__ a4 = reinterpret_cast<const u32x4*>(adj);
+    auto lean_test = [&](uint32_t x) -> uint32_t {
+        const uint32_t h = bloom_mix(x), fw = s_bloom[h >> 18];
+        uint32_t t = (fw >> ((h >> 13) & 31u)) & (fw >> ((h >> 8) & 31u));
+        if (WHARF_BLOOM_K > 2) t &= fw >> ((h >> 3) & 31u);
+        return t & 1u;
+    };
     // kInEdgeLoads 16-B loads per thread in flight (one left the pass latency-bound at 8 MB in flight;
     // configs[3] pool, 10.2 GB: 1 / 2 / 4 loads 3.00 / 2.75 / 2.65 ms, profiles/r02/in_edge_scan)
-    for (uint64_t q0 = g; q0 < n4; q0 += kInEdgeLoads * stride) {
+    for (uint32_t q0 = g; q0 < n4; q0 += kInEdgeLoads * stride) {
         u32x4 tv[kInEdgeLoads];
 #pragma unroll
         for (uint32_t u = 0; u < kInEdgeLoads; u++) {
-            const uint64_t q = q0 + u * stride;
+            const uint32_t q = q0 + u * stride;
             tv[u] = q < n4 ? __builtin_nontemporal_load(a4 + q) : u32x4{kGap, kGap, kGap, kGap};
         }
 #pragma unroll
         for (uint32_t u = 0; u < kInEdgeLoads; u++) {
             const u32x4 t = tv[u];
             // Bloom-test the four slots branch-free (kGap may pass: the exact test rejects it)
-            const uint32_t hit = (uint32_t)bloom_test_big(s_bloom, t.x) | (uint32_t)bloom_test_big(s_bloom, t.y) << 1 |
-                                 (uint32_t)bloom_test_big(s_bloom, t.z) << 2 | (uint32_t)bloom_test_big(s_bloom, t.w) << 3;
+            const uint32_t hit = lean_test(t.x) | lean_test(t.y) << 1 | lean_test(t.z) << 2 | lean_test(t.w) << 3;
             if (hit) {
                 const uint64_t q = q0 + u * stride;
                 for (uint32_t j = 0; j < 4; j++)
@@ -2386,9 +2393,10 @@ __global__ __launch_bounds__(1024, 8) void k_patch_in_edges(const uint32_t* __re
             }
         }
     }
-    if (g < slots - 4 * n4) {   // the pool's last < 4 slots
-        const uint32_t x = adj[4 * n4 + g];
-        if (bloom_test_big(s_bloom, x)) patch_slot(x, 4 * n4 + g, bitmap, vrec, erec, rs);
+    if (g < slots - 4 * (uint64_t)n4) {   // the pool's last < 4 slots
+        const uint64_t e = 4 * (uint64_t)n4 + g;
+        const uint32_t x = adj[e];
+        if (bloom_test_big(s_bloom, x)) patch_slot(x, e, bitmap, vrec, erec, rs);
     }
 }
 

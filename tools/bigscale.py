@@ -103,7 +103,7 @@ def main():
         del ref
     del off, adj, deg
     out = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device="cuda:0")
-    lat, gms, wms, affs, steps, inits, passes = [], [], [], [], [], [], []
+    lat, gms, wms, affs, steps, inits, passes, ies = [], [], [], [], [], [], [], []
     for b in range(a.batches):
         batch = W.generate_batch_of_edges(5000, n, b, False, False)
         for ins in ((True, False) if a.mixed else (True,)):
@@ -117,7 +117,9 @@ def main():
             steps.append(s2["steps"])
             inits.append(s2["last_anchor_inits"])
             passes.append(s2["last_rewalk_passes"])
-        print(f"batch {b}: {lat[-1]:.1f} ms (graph {gms[-1]:.1f}, re-walk {wms[-1]:.1f}), affected {affs[-1]}, "
+            ies.append(s2["last_csr_move_ms"])
+        print(f"batch {b}: {lat[-1]:.1f} ms (graph {gms[-1]:.1f} incl. in-edge scan {ies[-1]:.2f}, re-walk {wms[-1]:.1f}), "
+              f"affected {affs[-1]}, "
               f"steps {steps[-1]}, anchor inits {inits[-1]}, passes {passes[-1]}, m {g.number_of_edges()}", flush=True)
         if b == 0:
             m1 = g.memory_footprint(verbose=False)
