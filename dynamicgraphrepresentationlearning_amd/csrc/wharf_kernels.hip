@@ -904,16 +904,37 @@ __device__ __forceinline__ void filter_to_lds(const WalkArgs& a, uint32_t* s_blo
     __syncthreads();
 }
 
-template <int FB = 0>
+// LEAN (round 3, profiles/r03/scan_kernels): the filter bits tested as shifts of the
+// word and the walk's end found from the chunk's last position (kSent fills the
+// rest of a row once its walk ends): ~11 instead of ~17 VALU per position
+#ifndef WHARF_CHUNK_LEAN
+#define WHARF_CHUNK_LEAN 1
+#endif
+template <int FB = 0, bool LEAN = WHARF_CHUNK_LEAN != 0>
 __device__ __forceinline__ void chunk_issue(const WalkArgs& a, const uint32_t* s_bloom, const uint32_t (&x)[kScanChunk],
                                             uint32_t cnt, ChunkTest& t)
 {
     t.mask = 0;
     t.end = cnt;
+    if constexpr (LEAN) {
 #pragma unroll
-    for (uint32_t j = 0; j < kScanChunk; j++) {
-        t.mask |= (uint32_t)bloom_test_fb<FB>(s_bloom, x[j]) << j;
-        if (x[j] == kSent && j < t.end) t.end = j;
+        for (uint32_t j = 0; j < kScanChunk; j++) {
+            const uint32_t h = bloom_mix(x[j]), fw = s_bloom[h >> (20 - FB)];
+            uint32_t b = (fw >> ((h >> 13) & 31u)) & (fw >> ((h >> 8) & 31u));
+            if (WHARF_BLOOM_K > 2) b &= fw >> ((h >> 3) & 31u);
+            t.mask |= (b & 1u) << j;
+        }
+        if ((cnt == kScanChunk ? x[kScanChunk - 1] : chunk_pick(x, cnt - 1)) == kSent) {
+#pragma unroll
+            for (int j = (int)kScanChunk - 1; j >= 0; j--)
+                if (x[j] == kSent && (uint32_t)j < cnt) t.end = (uint32_t)j;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < kScanChunk; j++) {
+            t.mask |= (uint32_t)bloom_test_fb<FB>(s_bloom, x[j]) << j;
+            if (x[j] == kSent && j < t.end) t.end = j;
+        }
     }
     if (t.end < 32) t.mask &= (1u << t.end) - 1u;
 #if WHARF_SCAN_BATCH

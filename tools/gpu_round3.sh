@@ -37,6 +37,11 @@ for s in "$@"; do
     c4w1)   step c4_n2v_wpv1_shard8 600 python tools/bigscale.py --model node2vec --wpv 1 --batches 3 --mixed --no-oracle --shard 8 ;;
     c3shard8) step c3_shard8 900 python tools/bigscale.py --scale 25 --samples 1200000000 --wpv 10 --batches 5 --shard 8 ;;
     readout) step walk_readout 400 tools/walk_readout 20000 41943040 ;;
+    c4pmc)  C4="python3 tools/bigscale.py --model node2vec --wpv 10 --batches 2 --mixed --no-oracle --shard 8"
+            R="k_rewalk_sorted|k_rewalk_plan|k_anchor|k_patch_in_edges|k_walk"
+            step c4_trace 600 rocprofv3 --kernel-trace --stats --kernel-include-regex "$R" --output-format csv -d gpurun_out/r3/c4_trace -o run -- $C4
+            step c4_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$R" --output-format csv -d gpurun_out/r3/c4_fetch -o run -- $C4
+            step c4_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$R" --output-format csv -d gpurun_out/r3/c4_write -o run -- $C4 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
