@@ -2371,6 +2371,11 @@ __device__ __forceinline__ void patch_slot(uint32_t t, uint64_t e, const uint32_
 #define WHARF_INEDGE_LOADS 4
 #endif
 constexpr uint32_t kInEdgeLoads = WHARF_INEDGE_LOADS;
+// Round 3: the filter test of the thread's four 16-B loads first, then one
+// wave-uniform branch to the positives (round 2 branched per load: configs[3]
+// pass 2.65-2.73 -> 2.32-2.38 ms with the lean test).  A two-pass form that
+// listed the positives' slots and settled them after the stream was slower
+// (2.93-3.03 vs 2.52-2.56 ms, profiles/r03/in_edge_scan).
 __global__ __launch_bounds__(1024, 8) void k_patch_in_edges(const uint32_t* __restrict__ adj, uint64_t slots,
                                                         const uint32_t* __restrict__ bitmap,
                                                         const uint32_t* __restrict__ bloom_big,
@@ -2402,16 +2407,16 @@ __global__ __launch_bounds__(1024, 8) void k_patch_in_edges(const uint32_t* __re
             const uint32_t q = q0 + u * stride;
             tv[u] = q < n4 ? __builtin_nontemporal_load(a4 + q) : u32x4{kGap, kGap, kGap, kGap};
         }
+        uint32_t hits = 0;   // 4 bits per load
 #pragma unroll
         for (uint32_t u = 0; u < kInEdgeLoads; u++) {
             const u32x4 t = tv[u];
-            // Bloom-test the four slots branch-free (kGap may pass: the exact test rejects it)
-            const uint32_t hit = lean_test(t.x) | lean_test(t.y) << 1 | lean_test(t.z) << 2 | lean_test(t.w) << 3;
-            if (hit) {
-                const uint64_t q = q0 + u * stride;
-                for (uint32_t j = 0; j < 4; j++)
-                    if ((hit >> j) & 1u) patch_slot(t[j], 4 * q + j, bitmap, vrec, erec, rs);
-            }
+            hits |= (lean_test(t.x) | lean_test(t.y) << 1 | lean_test(t.z) << 2 | lean_test(t.w) << 3) << (4 * u);
+        }
+        if (!__any(hits != 0)) continue;
+        for (uint32_t m = hits; m; m &= m - 1u) {
+            const uint32_t b = (uint32_t)__builtin_ctz(m);
+            patch_slot(tv[b >> 2][b & 3u], 4 * (uint64_t)(q0 + (b >> 2) * stride) + (b & 3u), bitmap, vrec, erec, rs);
         }
     }
     if (g < slots - 4 * (uint64_t)n4) {   // the pool's last < 4 slots
