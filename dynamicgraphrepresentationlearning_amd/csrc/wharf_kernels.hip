@@ -1163,114 +1163,177 @@ __global__ __launch_bounds__(1024, 8) void k_rewalk_scan_big(WalkArgs a)
 // three bit tests as shifts of the word (7) and the mask bit (2); per chunk:
 // the walk-end test on the last position only (a walk that ends leaves kSent
 // in the rest of its row), the bitmap word of the first positive only, and
-// the 16 row loads from one buffer descriptor per chunk with the row offsets
+// the 16 row loads from two buffer descriptors per chunk with the row offsets
 // in SGPRs (1 SALU + 1 load per row, no per-row branch), issued after that
 // word's load so the wait for it leaves the rows in flight.  A false
 // positive (~0.1 % of positions with the 64-KiB filter) falls back to the
-// chunk's next positive, re-read from HBM.  Needs 15 * 4 * W < 2^32 (the host
-// uses k_rewalk_scan_big beyond).
+// chunk's next positive, re-read from HBM.  Needs 7 * 4 * W < 2^32 (the host
+// uses k_rewalk_scan_big / k_rewalk_plan beyond).
+constexpr uint64_t kLeanMaxW = ((1ull << 32) - 1) / 28;
 template <bool NTL>
 __device__ __forceinline__ void lean_chunk(const uint32_t* wb, uint32_t r0, uint32_t L, uint64_t W, uint32_t voff,
                                            uint32_t (&Y)[kScanChunk])
 {
     // always 16 loads and no branch (the compiler can then count them); rows
-    // past the walk length re-read the last row (only a partial last chunk)
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(wb + (uint64_t)r0 * W), 0, 0xFFFFFFFF,
-                                                                        kRowRsrcFlags);
-    const uint32_t w4 = (uint32_t)W * 4u, top = L - 1 - r0;
+    // past the walk length re-read the last row (only a partial last chunk).
+    // Rows r0..r0+7 and r0+8..r0+15 from one descriptor each (offsets < 7 rows)
+    const uint32_t w4 = (uint32_t)W * 4u, last = L - 1;
+    const uint32_t b1 = min(r0 + 8, last);
+    const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)(wb + (uint64_t)r0 * W), 0, 0xFFFFFFFF,
+                                                                         kRowRsrcFlags);
+    const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)(wb + (uint64_t)b1 * W), 0, 0xFFFFFFFF,
+                                                                         kRowRsrcFlags);
 #pragma unroll
-    for (uint32_t j = 0; j < kScanChunk; j++)
-        Y[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, (j < top ? j : top) * w4, NTL ? 2 : 0);
+    for (uint32_t j = 0; j < kScanChunk; j++) {
+        const uint32_t row = min(r0 + j, last);
+        if (j < 8) Y[j] = __builtin_amdgcn_raw_buffer_load_b32(rs0, voff, (row - r0) * w4, NTL ? 2 : 0);
+        else Y[j] = __builtin_amdgcn_raw_buffer_load_b32(rs1, voff, (row - b1) * w4, NTL ? 2 : 0);
+    }
+}
+
+// The rewalk point of the lane's walk (column `lane` of the wave's 64 columns at wb).
+template <bool NTL>
+__device__ __forceinline__ uint32_t lean_point(const WalkArgs& a, const uint32_t* s_bloom, const uint32_t* wb,
+                                               uint32_t lane)
+{
+    constexpr uint32_t C = kScanChunk;
+    const uint64_t W = a.W;
+    const uint32_t L = a.L;
+    // one chunk buffer: the chunk is dead once its first positive is picked,
+    // so the next chunk's loads reuse its registers
+    uint32_t X[C];
+    lean_chunk<NTL>(wb, 0, L, W, lane * 4, X);
+    uint32_t p = kNoRewalk;
+    bool scanning = true;
+    uint32_t mask, x0, j0, w0;
+    bool ended;
+    // the filter test of chunk c0 and the bitmap word of its first positive
+    auto test = [&](uint32_t c0) {
+        const uint32_t cnt = min(C, L - c0);
+        mask = 0;
+        ended = false;
+        if (scanning) {
+#pragma unroll
+            for (uint32_t j = 0; j < C; j++) {
+                const uint32_t h = bloom_mix(X[j]);
+                const uint32_t fw = s_bloom[h >> 18];
+                // bloom_bits(h) all set in fw: the three bits tested in place
+                uint32_t t = (fw >> ((h >> 13) & 31u)) & (fw >> ((h >> 8) & 31u));
+                if (WHARF_BLOOM_K > 2) t &= fw >> ((h >> 3) & 31u);
+                mask |= (t & 1u) << j;
+            }
+            if (cnt < C) mask &= (1u << cnt) - 1u;
+            const uint32_t last = cnt == C ? X[C - 1] : chunk_pick(X, cnt - 1);
+            if (last == kSent) {   // the walk ends in this chunk: positives stop at its end
+                ended = true;
+                uint32_t e = cnt;
+#pragma unroll
+                for (int j = (int)C - 1; j >= 0; j--)
+                    if (X[j] == kSent) e = (uint32_t)j;
+                mask &= (1u << e) - 1u;
+            }
+        }
+        x0 = 0, j0 = 0, w0 = 0;
+        if (mask) {
+            j0 = (uint32_t)__builtin_ctz(mask);
+            x0 = chunk_pick(X, j0);
+            w0 = a.bitmap[x0 >> 5];
+        }
+    };
+    // settle chunk c0 from its first positive's word
+    auto settle = [&](uint32_t c0) {
+        if (mask) {
+            bool hit = (w0 >> (x0 & 31u)) & 1u;
+            while (!hit) {   // a false positive: the next one, re-read from HBM (rare)
+                mask &= mask - 1u;
+                if (!mask) break;
+                j0 = (uint32_t)__builtin_ctz(mask);
+                x0 = walk_load<false>(wb + (uint64_t)(c0 + j0) * W + lane);
+                hit = (a.bitmap[x0 >> 5] >> (x0 & 31u)) & 1u;
+            }
+            if (hit) {
+                p = c0 + j0;
+                scanning = false;
+            }
+        }
+        if (ended) scanning = false;
+    };
+    uint32_t c0 = 0;
+    for (; c0 + C < L; c0 += C) {   // chunks with a successor: its 16 loads, unconditional
+        test(c0);
+        lean_chunk<NTL>(wb, c0 + C, L, W, lane * 4, X);
+        settle(c0);
+        if (!__any(scanning)) return p;
+    }
+    test(c0);   // the last chunk
+    settle(c0);
+    return p;
 }
 
 template <bool NTL>
 __global__ __launch_bounds__(1024, 8) void k_rewalk_scan_lean(WalkArgs a)
 {
-    constexpr uint32_t C = kScanChunk;
     __shared__ uint32_t s_bloom[kBigBloomWords];
     filter_to_lds<2>(a, s_bloom);
-    const uint64_t W = a.W;
-    const uint32_t L = a.L;
-    const XcdRange xr = xcd_range(W);
+    const XcdRange xr = xcd_range(a.W);
     const uint32_t lane = __lane_id();
     const uint32_t xend = (uint32_t)xr.end, xstride = (uint32_t)xr.stride;
     for (uint32_t li = (uint32_t)xr.first; li < xend; li += xstride) {
         const uint32_t* __restrict__ wb = a.walks + __builtin_amdgcn_readfirstlane(li - lane);
-        // one chunk buffer: the chunk is dead once its first positive is picked,
-        // so the next chunk's loads reuse its registers
-        uint32_t X[C];
-        lean_chunk<NTL>(wb, 0, L, W, lane * 4, X);
+        a.aff[li] = (uint8_t)lean_point<NTL>(a, s_bloom, wb, lane);
+    }
+}
+
+// k_rewalk_plan on the lean scan (round 3): 1024-thread workgroups (the 64-KiB
+// filter, two per CU), four 256-walk blocks per step, each binned and listed
+// exactly as k_rewalk_plan does it.
+template <bool NTL>
+__global__ __launch_bounds__(1024, 8) void k_rewalk_plan_lean(WalkArgs a)
+{
+    __shared__ uint32_t s_bloom[kBigBloomWords];
+    __shared__ uint32_t s_bin[4][256];                     // count, then cursor, per rewalk point (255: none)
+    __shared__ uint32_t s_wsum[4][kWavesPerBlock];
+    __shared__ unsigned long long s_ticket[4];
+    filter_to_lds<2>(a, s_bloom);
+    if (blockDim.x != 1024) __builtin_trap();              // four 256-walk blocks, one bin per thread
+    const uint64_t W = a.W;
+    const uint32_t L = a.L, t = threadIdx.x, sb = t >> 8, tl = t & 255, lane = __lane_id(), wv = tl >> 6;
+    for (uint64_t base = (uint64_t)blockIdx.x * 1024; base < W; base += (uint64_t)gridDim.x * 1024) {
+        const uint64_t li = base + t;
         uint32_t p = kNoRewalk;
-        bool scanning = true;
-        uint32_t mask, x0, j0, w0;
-        bool ended;
-        // the filter test of chunk c0 and the bitmap word of its first positive
-        auto test = [&](uint32_t c0) {
-            const uint32_t cnt = min(C, L - c0);
-            mask = 0;
-            ended = false;
-            if (scanning) {
+        if (li < W) p = lean_point<NTL>(a, s_bloom, a.walks + uniform64(li - lane), lane);
+        if (li < W) a.aff[li] = (uint8_t)p;
+        if (a.scan_only) continue;
+        const uint32_t key = (li < W && p + 1 < L) ? p : 255u;   // re-walking: something after the point
+        s_bin[sb][tl] = 0;
+        __syncthreads();
+        atomicAdd(&s_bin[sb][key], 1u);
+        __syncthreads();
+        const uint32_t c = s_bin[sb][tl];
+        uint32_t incl = c;                                 // exclusive scan of the block's 256 bins
 #pragma unroll
-                for (uint32_t j = 0; j < C; j++) {
-                    const uint32_t h = bloom_mix(X[j]);
-                    const uint32_t fw = s_bloom[h >> 18];
-                    // bloom_bits(h) all set in fw: the three bits tested in place
-                    uint32_t t = (fw >> ((h >> 13) & 31u)) & (fw >> ((h >> 8) & 31u));
-                    if (WHARF_BLOOM_K > 2) t &= fw >> ((h >> 3) & 31u);
-                    mask |= (t & 1u) << j;
-                }
-                if (cnt < C) mask &= (1u << cnt) - 1u;
-                const uint32_t last = cnt == C ? X[C - 1] : chunk_pick(X, cnt - 1);
-                if (last == kSent) {   // the walk ends in this chunk: positives stop at its end
-                    ended = true;
-                    uint32_t e = cnt;
-#pragma unroll
-                    for (int j = (int)C - 1; j >= 0; j--)
-                        if (X[j] == kSent) e = (uint32_t)j;
-                    mask &= (1u << e) - 1u;
-                }
-            }
-            x0 = 0, j0 = 0, w0 = 0;
-            if (mask) {
-                j0 = (uint32_t)__builtin_ctz(mask);
-                x0 = chunk_pick(X, j0);
-                w0 = a.bitmap[x0 >> 5];
-            }
-        };
-        // settle chunk c0 from its first positive's word
-        auto settle = [&](uint32_t c0) {
-            if (mask) {
-                bool hit = (w0 >> (x0 & 31u)) & 1u;
-                while (!hit) {   // a false positive: the next one, re-read from HBM (rare)
-                    mask &= mask - 1u;
-                    if (!mask) break;
-                    j0 = (uint32_t)__builtin_ctz(mask);
-                    x0 = walk_load<false>(wb + (uint64_t)(c0 + j0) * W + lane);
-                    hit = (a.bitmap[x0 >> 5] >> (x0 & 31u)) & 1u;
-                }
-                if (hit) {
-                    p = c0 + j0;
-                    scanning = false;
-                }
-            }
-            if (ended) scanning = false;
-        };
-        uint32_t c0 = 0;
-        bool done = false;
-        for (; c0 + C < L; c0 += C) {   // chunks with a successor: its 16 loads, unconditional
-            test(c0);
-            lean_chunk<NTL>(wb, c0 + C, L, W, lane * 4, X);
-            settle(c0);
-            if (!__any(scanning)) {
-                done = true;
-                break;
-            }
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+            if ((int)lane >= o) incl += y;
         }
-        if (!done) {   // the last chunk
-            test(c0);
-            settle(c0);
+        if (lane == 63) s_wsum[sb][wv] = incl;
+        __syncthreads();
+        uint32_t before = 0;
+        for (uint32_t w = 0; w < wv; w++) before += s_wsum[sb][w];
+        s_bin[sb][tl] = before + incl - c;
+        __syncthreads();
+        const uint32_t nact = s_bin[sb][255];              // entries ranked before the "none" bin
+        if (tl == 0) s_ticket[sb] = nact ? atomicAdd(a.counters + 2, (1ull << 40) | nact) : 0ull;
+        __syncthreads();
+        const uint64_t blk = (base >> 8) + sb;
+        if (tl == 0 && a.bdesc && (blk << 8) < W) a.bdesc[blk] = (s_ticket[sb] & kListMask) | ((uint64_t)nact << 40);
+        if (key != 255u) {
+            const uint32_t rank = atomicAdd(&s_bin[sb][key], 1u);
+            const uint64_t tk = s_ticket[sb];
+            const uint32_t at = ((tk >> 40) & 1u) ? nact - 1 - rank : rank;
+            a.defer[(tk & kListMask) + at] = li | ((uint64_t)p << 56);
         }
-        a.aff[li] = (uint8_t)p;
+        __syncthreads();                                   // s_bin / s_ticket are reused
     }
 }
 
@@ -1774,10 +1837,19 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
     const dim3 grid(rewalk ? std::min<uint64_t>((a.W + 255) / 256, (uint64_t)cu_count() * 8) : walk_grid(a.W)),
         block(256);
     const dim3 lgrid(list_grid());
+    // node2vec plan on the lean scan (WHARF_PLAN_KERNEL=chunked: k_rewalk_plan, round 2)
+    const char* pk = getenv("WHARF_PLAN_KERNEL");
+    const bool plan_lean = !(pk && std::string(pk) == "chunked") && a.W <= kLeanMaxW;
+    const dim3 pgrid((unsigned)std::min<uint64_t>((a.W + 1023) / 1024, (uint64_t)cu_count() * 2));
 #define WHARF_LAUNCH(M, D)                                                                   \
     do {                                                                                     \
         if (rewalk && M == kNode2Vec) {                                                      \
-            hipLaunchKernelGGL(k_rewalk_plan, grid, block, 0, s, a);                         \
+            if (plan_lean) {                                                                 \
+                if (a.nt_rows) hipLaunchKernelGGL(k_rewalk_plan_lean<true>, pgrid, dim3(1024), 0, s, a); \
+                else hipLaunchKernelGGL(k_rewalk_plan_lean<false>, pgrid, dim3(1024), 0, s, a);  \
+            } else {                                                                         \
+                hipLaunchKernelGGL(k_rewalk_plan, grid, block, 0, s, a);                     \
+            }                                                                                \
             if (!a.scan_only && !a.park) { /* park: the host runs the passes */              \
                 if (a.bdesc) hipLaunchKernelGGL((k_rewalk_block<M>), lgrid, block, 0, s, a);     \
                 else if (flat_list()) hipLaunchKernelGGL((k_rewalk_list<M, D>), lgrid, block, 0, s, a); \
@@ -1809,14 +1881,14 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
     }
     if (rewalk && a.scan_only && chunked) {
         // WHARF_SCAN_KERNEL (A/B and tests): lean (default) = k_rewalk_scan_lean, 64-KiB
-        // filter, where 15 * 4 * W fits 32 bits; big = k_rewalk_scan_big (round 2, also lean's
+        // filter, where 7 * 4 * W fits 32 bits; big = k_rewalk_scan_big (round 2, also lean's
         // fallback); WHARF_SCAN_SMALL_BLOOM=1: k_rewalk_chunked<false> with the 16-KiB filter
         const char* sb = getenv("WHARF_SCAN_SMALL_BLOOM");
         const char* sk = getenv("WHARF_SCAN_KERNEL");
         const bool small = sb && atoi(sb), big = sk && std::string(sk) == "big";
         const dim3 bgrid((std::max<unsigned>(std::min<uint64_t>((a.W + 1023) / 1024, (uint64_t)cu_count() * 2), kXcds) /
                           kXcds) * kXcds);
-        if (!small && !big && 15ull * 4ull * a.W < (1ull << 32)) {
+        if (!small && !big && a.W <= kLeanMaxW) {
             if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_scan_lean<true>), bgrid, dim3(1024), 0, s, a);
             else hipLaunchKernelGGL((k_rewalk_scan_lean<false>), bgrid, dim3(1024), 0, s, a);
             return;
