@@ -1003,8 +1003,13 @@ __device__ __forceinline__ XcdRange xcd_range(uint64_t W)
 #ifndef WHARF_SCAN_ONLY_WAVES_EU
 #define WHARF_SCAN_ONLY_WAVES_EU 8
 #endif
+#ifndef WHARF_COPY_WAVES
+#define WHARF_COPY_WAVES 1   // A/B: minimum waves/SIMD of the copy (1 = the compiler's choice; the 32-KiB
+                             // filter caps it at 5 by LDS; 16-KiB filter forced to 6: 100 B spilled, 16 vs
+                             // 7.2 ms, profiles/r03/copy_lean/copy_waves.txt)
+#endif
 template <bool COPY, bool NTL, int FB = 0>
-__global__ __launch_bounds__(256, COPY ? 1 : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArgs a)
+__global__ __launch_bounds__(256, COPY ? WHARF_COPY_WAVES : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArgs a)
 {
     constexpr uint32_t C = kScanChunk;
     __shared__ uint32_t s_bloom[kBloomWords << FB];
