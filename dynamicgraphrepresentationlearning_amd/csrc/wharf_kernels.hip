@@ -12,6 +12,7 @@
 //   bitmap[n/32]   batch-source set for the rewalk-point scan, + its Bloom filter
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "wharf_kernels.h"
 
