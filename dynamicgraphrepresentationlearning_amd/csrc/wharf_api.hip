@@ -536,6 +536,8 @@ struct wharf_handle {
         a.model = cfg.model; a.init = cfg.sampler_init; a.det = cfg.deterministic;
         const char* ns = getenv("WHARF_NO_SURE_SKIP");   // A/B: initialise every uncached anchor a step meets
         a.no_sure = ns && atoi(ns) ? 1 : 0;
+        const char* ls = getenv("WHARF_N2V_LANE_SORT");   // A/B and tests: 0 = list order
+        a.lane_sort = ls && *ls ? (atoi(ls) != 0) : 1;
         return a;
     }
 

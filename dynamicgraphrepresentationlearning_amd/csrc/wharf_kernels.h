@@ -57,6 +57,7 @@ struct WalkArgs {
     int nt_rows;                 // chunked scans: non-temporal walk-matrix row loads (most walks re-walk)
     int park;                    // node2vec MH re-walk by passes (k_rewalk_park / k_park_init), run by the host
     int no_sure;                 // A/B: initialise every uncached anchor a step meets (no sure-accept skip)
+    int lane_sort;               // node2vec sorted re-walk: a wave's 64 list entries in column order
 };
 
 constexpr uint64_t kListMask = (1ull << 40) - 1;   // counters[2]: tickets << 40 | re-walk list entries

@@ -1470,6 +1470,26 @@ __global__ __launch_bounds__(256) WHARF_SCAN_WAVES void k_rewalk_plan(WalkArgs a
     }
 }
 
+// Sort a wave's 64 re-walk list entries (walk | point << 56; ~0 = none) by walk
+// (column), ascending, so the nones end up last: bitonic over the lanes.
+__device__ __forceinline__ uint64_t wave_sort_entries(uint64_t ent)
+{
+    const uint32_t lane = __lane_id();
+    // key: the walk in the high bits, the point in the low byte (a none stays the largest)
+    uint64_t key = ent == ~0ull ? ~0ull : ((ent & ((1ull << 56) - 1)) << 8) | (ent >> 56);
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)(key >> 32), (int)j, 64) << 32) |
+                                   (uint32_t)__shfl_xor((int)(uint32_t)key, (int)j, 64);
+            const bool up = (lane & k) == 0, low = (lane & j) == 0;
+            key = (up == low) ? (key < other ? key : other) : (key < other ? other : key);
+        }
+    }
+    return key == ~0ull ? ~0ull : (key >> 8) | ((key & 0xFFull) << 56);
+}
+
 // (105 VGPRs, 4 waves/SIMD; forcing 5 spills 12 B and measured no faster:
 // configs[2] node2vec batch 65.4 vs 63.6 ms)
 template <int MODEL, bool DET>
@@ -1483,14 +1503,19 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     for (uint64_t c0 = wave * 64; c0 < cnt; c0 += nwaves * 64) {
         const uint64_t e = c0 + __lane_id();
-        const bool active = e < cnt;
+        // the wave's 64 entries (walks of one block at nearly the same rewalk point) in
+        // column order (round 3): lane order does not change what a wave computes (each
+        // walk's draws depend only on its id), but ascending columns let the row stores of
+        // neighbouring lanes merge; a bitonic sort over the wave, 21 shuffle steps
+        uint64_t ent = e < cnt ? a.defer[e] : ~0ull;
+        if (a.lane_sort) ent = wave_sort_entries(ent);
+        const bool active = ent != ~0ull;
         uint64_t li = 0;
         uint32_t p = L, wlo = 0, whi = 0;
         const uint64_t* __restrict__ rt = nullptr;
         Walker w;
         w.rc.deg = 0;
         if (active) {
-            const uint64_t ent = a.defer[e];
             li = ent & ((1ull << 56) - 1);
             p = (uint32_t)(ent >> 56);
             const uint64_t r = li / a.n_loc;
