@@ -759,6 +759,11 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
             // kMemoPad words before and after the table: k_rewalk_chunked reads whole
             // chunks around a row (values outside the row are never written)
             h->memo.ensure(((uint64_t)h->wpv * k * stride4 + 2 * kMemoPad) * 4);
+            // every non-source kNoSource: the copy settles a Bloom positive by its index alone
+            // (WHARF_COPY_BITMAP=1, A/B: by the bitmap word, then the index)
+            const char* cbm = getenv("WHARF_COPY_BITMAP");
+            a.src_exact = !(cbm && atoi(cbm));
+            if (a.src_exact) HIPCHK(hipMemsetAsync(h->srcidx.p, 0xFF, std::max<uint64_t>(h->n, 1) * 4, s));
             launch_src_index(h->runs.as<RunInfo>(), k, h->srcidx.as<uint32_t>(), s);
             a.memo = h->memo.as<uint32_t>() + kMemoPad;
             a.src_idx = h->srcidx.as<uint32_t>();

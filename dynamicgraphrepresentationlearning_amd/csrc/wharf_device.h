@@ -17,6 +17,7 @@ namespace wharf {
 constexpr uint32_t kSent = 0xFFFFFFFEu;        // wharfmh.h:282 (uint32 max - 1)
 constexpr uint32_t kAnchorNone = 0xFFFFFFFFu;  // MH anchor slot not initialised yet
 constexpr uint32_t kNoRewalk = 0xFFu;          // rewalk position "none"
+constexpr uint32_t kNoSource = 0xFFFFFFFFu;    // src_idx of a vertex that is not a batch source
 constexpr uint32_t kBloomWords = 4096;         // batch-source Bloom filter: 2^17 bits (16 KiB, LDS)
 constexpr uint32_t kGap = 0xFFFFFFFFu;         // unused slot of the slack-row pool (not a vertex id)
 

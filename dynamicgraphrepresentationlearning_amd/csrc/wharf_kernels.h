@@ -48,7 +48,7 @@ struct WalkArgs {
     uint64_t stab_mask;          //   buckets - 1
     // deterministic re-walk by suffix table (k_det_suffix + k_rewalk_chunked<true>), or memo == null
     uint32_t* memo;              // [wpv][k][memo_stride]: walk from batch source i in round r, new graph
-    const uint32_t* src_idx;     // [n]: index of a batch source in the run table (read for sources only)
+    const uint32_t* src_idx;     // [n]: index of a batch source in the run table (kNoSource elsewhere when src_exact)
     const RunInfo* runs;         // the batch's source runs
     uint64_t memo_k;             // sources (runs) in the batch
     uint32_t memo_stride;        // L rounded up to 4 (16-B aligned rows)
@@ -58,6 +58,7 @@ struct WalkArgs {
     int park;                    // node2vec MH re-walk by passes (k_rewalk_park / k_park_init), run by the host
     int no_sure;                 // A/B: initialise every uncached anchor a step meets (no sure-accept skip)
     int lane_sort;               // node2vec sorted re-walk: a wave's 64 list entries in column order
+    int src_exact;               // src_idx holds kNoSource for every non-source (the copy settles positives by it)
 };
 
 constexpr uint64_t kListMask = (1ull << 40) - 1;   // counters[2]: tickets << 40 | re-walk list entries

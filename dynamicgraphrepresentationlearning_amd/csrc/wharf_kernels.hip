@@ -911,7 +911,11 @@ __device__ __forceinline__ void filter_to_lds(const WalkArgs& a, uint32_t* s_blo
 #ifndef WHARF_CHUNK_LEAN
 #define WHARF_CHUNK_LEAN 1
 #endif
-template <int FB = 0, bool LEAN = WHARF_CHUNK_LEAN != 0>
+// IDX (the deterministic copy, round 3): the positives' source indices
+// (a.src_idx, kNoSource for every vertex that is not a batch source) instead
+// of their bitmap words: one read both settles a positive and names its
+// suffix-table row (the copy read the bitmap word, then the index)
+template <int FB = 0, bool LEAN = WHARF_CHUNK_LEAN != 0, bool IDX = false>
 __device__ __forceinline__ void chunk_issue(const WalkArgs& a, const uint32_t* s_bloom, const uint32_t (&x)[kScanChunk],
                                             uint32_t cnt, ChunkTest& t)
 {
@@ -940,17 +944,24 @@ __device__ __forceinline__ void chunk_issue(const WalkArgs& a, const uint32_t* s
     if (t.end < 32) t.mask &= (1u << t.end) - 1u;
 #if WHARF_SCAN_BATCH
 #pragma unroll
-    for (uint32_t j = 0; j < kScanChunk; j++) t.w[j] = ((t.mask >> j) & 1u) ? a.bitmap[x[j] >> 5] : 0u;
+    for (uint32_t j = 0; j < kScanChunk; j++) {
+        if constexpr (IDX) t.w[j] = ((t.mask >> j) & 1u) ? a.src_idx[x[j]] : kNoSource;
+        else t.w[j] = ((t.mask >> j) & 1u) ? a.bitmap[x[j] >> 5] : 0u;
+    }
 #endif
 }
 
+template <bool IDX = false>
 __device__ __forceinline__ uint32_t chunk_resolve(const WalkArgs& a, const uint32_t (&x)[kScanChunk], uint32_t cnt,
                                                   const ChunkTest& t, bool& ended)
 {
 #if WHARF_SCAN_BATCH
     uint32_t hit = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < kScanChunk; j++) hit |= ((t.w[j] >> (x[j] & 31u)) & 1u) << j;
+    for (uint32_t j = 0; j < kScanChunk; j++) {
+        if constexpr (IDX) hit |= (uint32_t)(t.w[j] != kNoSource) << j;
+        else hit |= ((t.w[j] >> (x[j] & 31u)) & 1u) << j;
+    }
     hit &= t.mask;
     if (hit) return (uint32_t)__builtin_ctz(hit);
 #else
@@ -1009,7 +1020,7 @@ __device__ __forceinline__ XcdRange xcd_range(uint64_t W)
                              // filter caps it at 5 by LDS; 16-KiB filter forced to 6: 100 B spilled, 16 vs
                              // 7.2 ms, profiles/r03/copy_lean/copy_waves.txt)
 #endif
-template <bool COPY, bool NTL, int FB = 0>
+template <bool COPY, bool NTL, int FB = 0, bool IDX = false>
 __global__ __launch_bounds__(256, COPY ? WHARF_COPY_WAVES : WHARF_SCAN_ONLY_WAVES_EU) WHARF_SCAN_WAVES void k_rewalk_chunked(WalkArgs a)
 {
     constexpr uint32_t C = kScanChunk;
@@ -1037,7 +1048,7 @@ __global__ __launch_bounds__(256, COPY ? WHARF_COPY_WAVES : WHARF_SCAN_ONLY_WAVE
             const bool was_scanning = scanning;
             const bool more = c0 + C < L;
             ChunkTest ct;
-            if (scanning) chunk_issue<FB>(a, s_bloom, cur, cnt, ct);
+            if (scanning) chunk_issue<FB, WHARF_CHUNK_LEAN != 0, COPY && IDX>(a, s_bloom, cur, cnt, ct);
             if (!COPY && more && scanning) {
                 // scan only: the next chunk's rows go out before the bitmap words
                 // are waited for (loads complete in order: the wait leaves them in flight)
@@ -1047,13 +1058,13 @@ __global__ __launch_bounds__(256, COPY ? WHARF_COPY_WAVES : WHARF_SCAN_ONLY_WAVE
             }
             if (scanning) {
                 bool ended = false;
-                const uint32_t j = chunk_resolve(a, cur, cnt, ct, ended);
+                const uint32_t j = chunk_resolve<COPY && IDX>(a, cur, cnt, ct, ended);
                 if (j < C) {
                     p = c0 + j;
                     scanning = false;
                     if (COPY) {
-                        const uint32_t x = chunk_pick(cur, j);
-                        row = a.memo + (r * a.memo_k + a.src_idx[x]) * a.memo_stride - p;
+                        const uint32_t sx = (COPY && IDX) ? chunk_pick(ct.w, j) : a.src_idx[chunk_pick(cur, j)];
+                        row = a.memo + (r * a.memo_k + sx) * a.memo_stride - p;
                     }
                 } else if (ended) {
                     scanning = false;
@@ -1904,6 +1915,9 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
         if (cb && atoi(cb)) {
             if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<true, true, 0>), mgrid, block, 0, s, a);
             else hipLaunchKernelGGL((k_rewalk_chunked<true, false, 0>), mgrid, block, 0, s, a);
+        } else if (a.src_exact) {   // the source index settles the positives (IDX)
+            if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<true, true, 1, true>), mgrid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_rewalk_chunked<true, false, 1, true>), mgrid, block, 0, s, a);
         } else {
             if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<true, true, 1>), mgrid, block, 0, s, a);
             else hipLaunchKernelGGL((k_rewalk_chunked<true, false, 1>), mgrid, block, 0, s, a);

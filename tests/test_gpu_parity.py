@@ -407,6 +407,8 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     monkeypatch.setenv("WHARF_SCAN_SMALL_BLOOM", "1" if path == "sorted/plain-rows" else "0")
     monkeypatch.setenv("WHARF_SCAN_KERNEL", "big" if path in ("flat/move", "block/move-lazy") else "lean")
     monkeypatch.setenv("WHARF_BLOOM_SATURATE", "1" if path in ("sorted/lazy-inits", "block/slack") else "0")
+    # deterministic copy: positives settled by the source index (default) or by the bitmap word first
+    monkeypatch.setenv("WHARF_COPY_BITMAP", "1" if path in ("flat/move", "sorted/repack") else "0")
     # node2vec sorted re-walk: a wave's entries in column order (default) or in list order
     monkeypatch.setenv("WHARF_N2V_LANE_SORT", "0" if path in ("sorted/plain-rows", "sorted/repack") else "1")
     # node2vec plan (rewalk points + the binned re-walk list): on the lean scan (default) or k_rewalk_plan
