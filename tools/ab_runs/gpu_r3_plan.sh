@@ -1,0 +1,19 @@
+#!/bin/bash
+# node2vec plan on the lean scan: parity, then configs[2] node2vec probe and configs[4] 1/8 shard (wpv 10),
+# lean vs chunked (k_rewalk_plan), alternated; plan kernel durations from a kernel trace of each probe.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r3plan; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -k "paths or rmat10 or edge_cases or extreme or batch_walk_update or stream" --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pt.log 2>&1
+rc=$?; grep -E "passed|failed" $O/pt.log | tail -2; [ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/pt.log | head; exit $rc; }
+export TMPDIR=/tmp
+for v in lean chunked lean chunked; do
+  export WHARF_PLAN_KERNEL=$v
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --kernel-include-regex "k_rewalk_plan|k_rewalk_sorted|k_rewalk_scan" --output-format csv -d $O/n2v_$v -o run -- python3 tools/rewalk_probe.py --model node2vec --batches 3 > $O/proben2v_$v.log 2>&1 || exit 6
+  echo "n2v $v: $(grep -v '^[WEI]2026' $O/proben2v_$v.log | tail -1)"
+done
+for v in lean chunked; do
+  export WHARF_PLAN_KERNEL=$v
+  timeout -k 10 500 python tools/bigscale.py --model node2vec --wpv 10 --batches 2 --mixed --no-oracle --shard 8 > $O/c4_$v.log 2>&1 || exit 7
+  echo "c4 $v: $(grep -E '^batch' $O/c4_$v.log | tr '\n' ' ' | cut -c1-420)"
+done
