@@ -538,6 +538,13 @@ struct wharf_handle {
         a.no_sure = ns && atoi(ns) ? 1 : 0;
         const char* ls = getenv("WHARF_N2V_LANE_SORT");   // A/B and tests: 0 = list order
         a.lane_sort = ls && *ls ? (atoi(ls) != 0) : 1;
+        // return-first inits (A/B path, WHARF_RET_FIRST=1; off by default: configs[4] shard re-walk
+        // 17.8-18.2 -> 17.1-17.3 ms at wpv 1 but 67-78 -> 73-82 ms at wpv 10, configs[2] +0.7 %,
+        // profiles/r03/retfirst) need the return to be the one heaviest class (p < 1, p < q) and
+        // proposals that need has_edge at all (q != 1)
+        const char* rf = getenv("WHARF_RET_FIRST");
+        a.ret_first = cfg.model == WHARF_NODE2VEC && !cfg.deterministic && cfg.sampler_init == WHARF_INIT_WEIGHT &&
+                      !a.no_sure && a.inv_q != 1.0f && a.inv_p > fmaxf(1.0f, a.inv_q) && rf && *rf && atoi(rf) != 0;
         return a;
     }
 

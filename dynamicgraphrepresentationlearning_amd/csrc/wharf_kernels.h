@@ -59,6 +59,7 @@ struct WalkArgs {
     int no_sure;                 // A/B: initialise every uncached anchor a step meets (no sure-accept skip)
     int lane_sort;               // node2vec sorted re-walk: a wave's 64 list entries in column order
     int src_exact;               // src_idx holds kNoSource for every non-source (the copy settles positives by it)
+    int ret_first;               // node2vec MH, WEIGHT, 1/p the unique heaviest weight: return-first inits (walk_step)
 };
 
 constexpr uint64_t kListMask = (1ull << 40) - 1;   // counters[2]: tickets << 40 | re-walk list entries

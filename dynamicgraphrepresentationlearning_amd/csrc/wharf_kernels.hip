@@ -208,7 +208,7 @@ constexpr uint32_t kInitRounds = WHARF_INIT_ROUNDS;   // proposals per active la
 constexpr uint32_t kWavesPerBlock = 4;                // every walk kernel runs 256-thread blocks
 
 struct InitReq {     // a lane's init, published for the wave
-    uint32_t cv, cdeg, cep, pv, pdeg;
+    uint32_t cv, cdeg, cep, pv, pdeg, tonly;
     uint64_t coff, poff, fd;
 };
 
@@ -216,9 +216,15 @@ struct InitReq {     // a lane's init, published for the wave
 // compiler from moving the per-init table accesses across the phases
 __device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_wave_barrier(); }
 
+// TONLY (return-first inits, WalkArgs::ret_first): a lane whose step is settled
+// whenever the anchor is not a return asks for its proposals' targets only; no
+// filter word or edge-hash bucket is read for them.  `resolved` comes back
+// false when none of the 21 proposals is the return (the anchor is then not
+// known, only that it weighs at most max(1, 1/q)); with a return among them the
+// anchor is the first return (the heaviest class when ret_first is set).
 template <uint32_t ROUNDS = kInitRounds>
 __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, const Row& rp, uint32_t& slot,
-                                 uint32_t& cls)
+                                 uint32_t& cls, bool tonly = false, bool* resolved = nullptr)
 {
     constexpr uint32_t kInitRounds = ROUNDS;
     __shared__ InitReq s_req[kWavesPerBlock][64];
@@ -232,7 +238,8 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
     const uint32_t cnt = (uint32_t)__popcll(mask), me = (uint32_t)__popcll(mask & below);
     const bool use_f = a.fpool && a.inv_q != 1.0f;
     if (need) {
-        s_req[wv][me] = InitReq{rc.v, rc.deg, rc.epoch, rp.v, rp.deg, rc.off, rp.off, use_f ? a.fdir[rp.v] : 0ull};
+        s_req[wv][me] = InitReq{rc.v, rc.deg, rc.epoch, rp.v, rp.deg, (uint32_t)tonly, rc.off, rp.off,
+                                use_f && !tonly ? a.fdir[rp.v] : 0ull};
         s_key[wv][me] = ~0u;
     }
     wave_lds_sync();
@@ -257,7 +264,7 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
 #pragma unroll
         for (uint32_t b = 0; b < kInitRounds; b++) {
             fw[b] = 0, fb[b] = 0;
-            if (t[b] < cnt && use_f && cv[b] != s_req[wv][t[b]].pv) {
+            if (t[b] < cnt && use_f && cv[b] != s_req[wv][t[b]].pv && !s_req[wv][t[b]].tonly) {
                 const uint64_t h = filt_hash(cv[b]);
                 fb[b] = filt_bits(h);
                 fw[b] = a.fpool[filt_word(s_req[wv][t[b]].fd, h)];
@@ -269,6 +276,7 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
             const InitReq q = s_req[wv][t[b]];
             uint32_t c;
             if (cv[b] == q.pv) c = 0;
+            else if (q.tonly) continue;        // only a return can settle a targets-only init
             else if (a.inv_q == 1.0f) c = 1;   // triangle and outward weigh the same
             else if (use_f && (fw[b] & fb[b]) != fb[b]) c = 2;   // filter negative: exact
             else c = has_edge(a, Row{q.pv, q.pdeg, 0u, q.poff}, cv[b]) ? 1 : 2;
@@ -279,6 +287,8 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
     wave_lds_sync();
     if (need) {
         const uint32_t key = s_key[wv][me];
+        if (resolved) *resolved = key != ~0u;
+        if (key == ~0u) return;   // targets-only, no return among the proposals
         const P4 r = philox4x32_10(rc.v, rp.v, (key >> 2) & 31, (rc.epoch << 4) | kStreamAnchor, a.key0, a.key1);
         slot = (uint32_t)pick32(r.x0, rc.deg);
         cls = key & 3;
@@ -286,16 +296,28 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
 }
 
 // The cached anchor of the walker's state, or need = true (no valid entry).
+// Class 3 is the return-first marker (walk_step): the state's 21 proposals hold
+// no return, the anchor itself is not known yet (need stays true, noret is set).
+constexpr uint32_t kClassNoReturn = 3;
+__device__ __forceinline__ uint64_t noreturn_entry(uint32_t epoch)
+{
+    return ((uint64_t)kClassNoReturn << 62) | ((uint64_t)epoch << 32) | 0xFFFFFFFEull;
+}
 __device__ __forceinline__ void anchor_lookup(const WalkArgs& a, const Row& rc, const Row& rp, const uint64_t* ac,
-                                              uint64_t anc, uint32_t& an, uint32_t& cls, bool& need)
+                                              uint64_t anc, uint32_t& an, uint32_t& cls, bool& need, bool& noret)
 {
     need = true;
+    noret = false;
     if (ac) {
         const uint32_t tag = (uint32_t)(anc >> 32) & 0x3FFFFFFFu;
         if (anc != kAnchorNone64 && tag >= rc.epoch) {
-            need = false;
-            an = (uint32_t)anc;
-            cls = (uint32_t)(anc >> 62);
+            if ((uint32_t)(anc >> 62) == kClassNoReturn) {
+                noret = true;
+            } else {
+                need = false;
+                an = (uint32_t)anc;
+                cls = (uint32_t)(anc >> 62);
+            }
         }
     }
 }
@@ -304,11 +326,17 @@ __device__ __forceinline__ void anchor_lookup(const WalkArgs& a, const Row& rc, 
 // cached.  Called by every active lane of the wave together (WEIGHT inits are
 // wave-cooperative); lanes with need = false pass an / cls through.
 __device__ __forceinline__ uint32_t anchor_fill(const WalkArgs& a, bool need, const Row& rc, const Row& rp,
-                                                uint64_t* ac, uint64_t anc, uint32_t an, uint32_t& cls, uint32_t& inits)
+                                                uint64_t* ac, uint64_t anc, uint32_t an, uint32_t& cls, uint32_t& inits,
+                                                bool tonly, bool& resolved)
 {
     inits += need;   // per lane; the kernel adds them up once (counters[7])
+    resolved = true;
     if (a.init == kInitWeight) {
-        anchor_init_wave(a, need, rc, rp, an, cls);
+        anchor_init_wave(a, need, rc, rp, an, cls, tonly, &resolved);
+        if (!resolved) {   // the anchor is not known; cache what is: no proposal returns
+            if (need && ac) *ac = noreturn_entry(a.epoch);
+            return an;
+        }
     } else if (need) {
         an = anchor_init(a, rc, rp, cls);
     }
@@ -367,7 +395,7 @@ __device__ __forceinline__ Row load_edge(const WalkArgs& a, uint64_t e, uint64_t
 // not cached and is needed for the decision is not initialised here; the step
 // returns with `parked` set and the walker unchanged, and k_park_init computes
 // the anchor with full waves before the walker resumes.
-template <int MODEL, bool DET, bool PARK = false>
+template <int MODEL, bool DET, bool PARK = false, bool RF = false>
 __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, const uint64_t* __restrict__ rt,
                                               uint32_t pos, uint32_t wlo, uint32_t whi, uint32_t ep, uint32_t& accepts,
                                               uint32_t& inits, bool* parked = nullptr)
@@ -394,8 +422,8 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
             const double u = u01(q.x1, q.x2);
             auto accept = [&](float wc, float wa) { return (wa < wc) || (u <= (double)wc / (double)wa); };
             uint32_t acls = 0, ai = 0;
-            bool need;
-            anchor_lookup(a, w.rc, w.rp, w.ac, w.anc, ai, acls, need);
+            bool need, noret;
+            anchor_lookup(a, w.rc, w.rp, w.ac, w.anc, ai, acls, need, noret);
             // The decision falls monotonically with w(a) and rises with w(c): a
             // candidate accepted against the heaviest class with its lightest
             // possible weight is accepted whatever the anchor is, so an anchor
@@ -406,22 +434,41 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
             const bool sure = need && !a.no_sure &&
                               accept(cand.v == w.rp.v ? a.inv_p : w_lightest_nonreturn(a), w_heaviest(a));
             const bool init = need && !sure;
+            bool resolved = true;
+            uint32_t ccls = 3;   // the candidate's class once probed, 3 = not probed
             if constexpr (PARK) {
                 if (init) {
                     *parked = true;
                     return 0;
                 }
             } else {
-                ai = anchor_fill(a, init, w.rc, w.rp, w.ac, w.anc, ai, acls, inits);
+                // Return-first (ret_first: the return 1/p is the unique heaviest class, WEIGHT
+                // inits).  The candidate's own class is probed first; when it is accepted against
+                // every non-return anchor (max(1, 1/q)), only a return among the 21 proposals could
+                // reject it, and a return needs no has_edge: the init reads its proposals' targets
+                // and none of prev's filter words or edge-hash buckets.  Exact (the decision falls
+                // monotonically with the anchor's weight).  When no proposal returns, the entry
+                // keeps that fact (kClassNoReturn), so the next walker whose candidate is settled
+                // by it needs no init at all.  (A return candidate is sure-accepted under ret_first.)
+                bool tonly = false, fill = init;
+                if (RF && a.ret_first && init) {
+                    ccls = cand.v == w.rp.v ? 0u : (has_edge(a, w.rp, cand.v) ? 1u : 2u);
+                    tonly = accept(class_weight(a, ccls), fmaxf(1.0f, a.inv_q));
+                    if (tonly && noret) fill = false;   // settled by the cached fact alone
+                }
+                ai = anchor_fill(a, fill, w.rc, w.rp, w.ac, w.anc, ai, acls, inits, tonly && !noret, resolved);
+                if (init && !fill) resolved = false;
             }
-            bool ok = true;   // proposing the anchor itself is always accepted
-            if (!sure && ai != ci) {
+            bool ok = true;   // proposing the anchor itself is always accepted (and an unresolved
+                              // targets-only init: the candidate wins against any non-return anchor)
+            if (!sure && resolved && ai != ci) {
                 const float wa = class_weight(a, acls);
                 if (cand.v == w.rp.v) {
                     ok = accept(a.inv_p, wa);
                 } else {
                     const bool ok_tri = accept(1.0f, wa), ok_out = accept(a.inv_q, wa);
-                    ok = ok_tri == ok_out ? ok_tri : (has_edge(a, w.rp, cand.v) ? ok_tri : ok_out);
+                    const bool tri = ok_tri == ok_out || (ccls != 3 ? ccls == 1 : has_edge(a, w.rp, cand.v));
+                    ok = tri ? ok_tri : ok_out;
                 }
             }
             accepts += ok;
@@ -1544,7 +1591,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
         for (uint32_t pos = first; pos < L; pos++) {
             uint32_t val = kSent;
             if (active && pos > p && w.rc.deg) {
-                val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
+                val = walk_step<MODEL, DET, false, true>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
                 steps++;
             }
             // the lanes are walks scattered over a block (sorted by rewalk point),
@@ -1622,7 +1669,7 @@ __global__ __launch_bounds__(256) void k_rewalk_block(WalkArgs a)
                 if (active && pos > p) {
                     uint32_t val = kSent;
                     if (w.rc.deg) {
-                        val = walk_step<MODEL, false>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, inits);
+                        val = walk_step<MODEL, false, false, true>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, inits);
                         steps++;
                     }
                     tile[j][li - base] = val;
@@ -1688,7 +1735,7 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
         if (pos < L) {
             uint32_t val = kSent;
             if (w.rc.deg) {
-                val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
+                val = walk_step<MODEL, DET, false, true>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
                 steps++;
             }
             walks[(uint64_t)pos * W + li] = val;
@@ -1774,7 +1821,7 @@ __global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* 
         if (has) {
             uint32_t val = kSent;
             const bool live = w.rc.deg != 0;   // a walk at a vertex without out-edges ends
-            if (live) val = walk_step<MODEL, false, PARK>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, inits, &park);
+            if (live) val = walk_step<MODEL, false, PARK, !PARK>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, inits, &park);
             if (!park) {
                 steps += live;
                 walks[(uint64_t)pos * W + li] = val;

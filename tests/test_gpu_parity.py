@@ -411,6 +411,9 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     monkeypatch.setenv("WHARF_COPY_BITMAP", "1" if path in ("flat/move", "sorted/repack") else "0")
     # node2vec sorted re-walk: a wave's entries in column order (default) or in list order
     monkeypatch.setenv("WHARF_N2V_LANE_SORT", "0" if path in ("sorted/plain-rows", "sorted/repack") else "1")
+    # node2vec WEIGHT inits of the re-walk: return-first (default: a step settled by any non-return
+    # anchor reads only its proposals' targets) or always the full init
+    monkeypatch.setenv("WHARF_RET_FIRST", "0" if path in ("sorted/plain-rows", "flat/slack-repack") else "1")
     # node2vec plan (rewalk points + the binned re-walk list): on the lean scan (default) or k_rewalk_plan
     monkeypatch.setenv("WHARF_PLAN_KERNEL", "chunked" if path in ("flat/move", "sorted/plain-rows", "park/repack-tail")
                        else "lean")
