@@ -34,15 +34,19 @@ def main():
                         sampler_init={"random": W.RANDOM, "burnin": W.BURNIN, "weight": W.WEIGHT}[a.init])
     g = W.WharfMH.from_rmat(n, a.samples, 2 * n, seed=2, config=cfg)
     g.generate_initial_random_walks()
-    res = {"scan_only_ms": [], "fused_ms": [], "affected": [], "steps": []}
+    # *_ms: the walk update alone (stats); *_total_ms: the whole insert call (CSR update + walk update +
+    # affected ids to the host), which is what an overlap of the two shows in
+    res = {"scan_only_ms": [], "fused_ms": [], "scan_only_total_ms": [], "fused_total_ms": [], "affected": [], "steps": []}
     for b in range(a.batches):
         batch = W.generate_batch_of_edges(5000, n, 100 + b, False, False)
         aff = g.insert_edges_batch(batch, apply_walk_updates=False)
         res["scan_only_ms"].append(g.stats()["last_walk_update_ms"])
+        res["scan_only_total_ms"].append(g.stats()["last_total_ms"])
         batch2 = W.generate_batch_of_edges(5000, n, 500 + b, False, False)
         aff2 = g.insert_edges_batch(batch2, apply_walk_updates=True)
         st = g.stats()
         res["fused_ms"].append(st["last_walk_update_ms"])
+        res["fused_total_ms"].append(st["last_total_ms"])
         res["affected"].append(len(aff2))
         res["steps"].append(st["steps"])
         print(f"batch {b}: scan-only {res['scan_only_ms'][-1]:.2f} ms ({len(aff)} affected), "
