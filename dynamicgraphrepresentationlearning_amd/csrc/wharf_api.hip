@@ -85,11 +85,6 @@ struct wharf_handle {
     int device = 0;
     hipStream_t s = nullptr;
     hipEvent_t ev[6] = {};
-    // the node2vec plan / rewalk-point scan of an update batch reads only the old walk matrix and
-    // the sources' bitmap, so it runs on s2 beside the CSR update (early_plan: launched, ev_plan marks it)
-    hipStream_t s2 = nullptr;
-    hipEvent_t ev_plan = nullptr;
-    bool early_plan = false;
     wharf_config cfg{};
     uint64_t n = 0, m = 0, lo = 0, hi = 0, n_loc = 0, W = 0;
     uint32_t L = 0, wpv = 0;
@@ -638,9 +633,7 @@ wharf_handle* new_handle(const wharf_config* cfg, uint64_t n, int device)
     h->W = h->n_loc * h->wpv;
     h->anchors = cfg->model == WHARF_NODE2VEC && !cfg->deterministic;
     HIPCHK(hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&h->s2, hipStreamNonBlocking));
     for (auto& e : h->ev) HIPCHK(hipEventCreate(&e));
-    HIPCHK(hipEventCreateWithFlags(&h->ev_plan, hipEventDisableTiming));
     // deterministic draw table: Random(r).lrand() for r < wpv (utility.h:157-206)
     std::vector<uint64_t> t((size_t)h->wpv * h->L);
     for (uint32_t r = 0; r < h->wpv; r++) {
@@ -659,7 +652,6 @@ void free_handle(wharf_handle* h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->s) (void)hipStreamSynchronize(h->s);
-    if (h->s2) (void)hipStreamSynchronize(h->s2);
     for (DevBuf* b : {&h->off, &h->adj, &h->deg, &h->cap, &h->vrec, &h->erec, &h->erec2, &h->ehash, &h->fdir, &h->fpool,
                       &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->walks, &h->aff, &h->rtab,
                       &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags, &h->chg, &h->cf,
@@ -669,9 +661,7 @@ void free_handle(wharf_handle* h)
     h->free_snaps();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
-    if (h->ev_plan) (void)hipEventDestroy(h->ev_plan);
     if (h->s) (void)hipStreamDestroy(h->s);
-    if (h->s2) (void)hipStreamDestroy(h->s2);
     delete h;
 }
 
@@ -747,70 +737,24 @@ void park_passes(wharf_handle* h, const WalkArgs& a)
 // 733-923) of every owned walk that holds a vertex of the bitmap; h->runs
 // holds the k sources (the deterministic suffix table is keyed by them), and
 // ev[1] marks the start of the walk update.
-// The walk-update fields the plan kernels read (shared by the early plan and walk_update).
-void plan_fields(wharf_handle* h, uint64_t k, uint32_t flags, WalkArgs& a)
-{
-    a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
-    // chunked scans: non-temporal row loads when most walks are expected to re-walk.  The
-    // share grows with k * L / n (RMAT batches: configs[2] 0.19 -> 81 % re-walk, NT loads
-    // win; configs[3] 1/8 shard 0.024 -> 32 %, they lose 35 %); WHARF_NT_ROWS=0/1 forces it
-    const char* ntr = getenv("WHARF_NT_ROWS");
-    a.nt_rows = ntr ? (atoi(ntr) != 0) : ((double)k * h->L >= 0.08 * (double)std::max<uint64_t>(h->n, 1));
-    if (a.model == kNode2Vec && !a.det) {   // k_rewalk_plan's compacted, sorted re-walk list
-        h->defer.ensure(h->W * 8);
-        a.defer = h->defer.as<uint64_t>();
-        const char* rwm = getenv("WHARF_N2V_REWALK");   // =block: k_rewalk_block (row-staged stores)
-        if (rwm && std::string(rwm) == "block" && !a.scan_only) {
-            h->bdesc.ensure(((h->W + 255) / 256) * 8);
-            a.bdesc = h->bdesc.as<uint64_t>();
-        }
-    }
-}
-
-// Counters zeroed, and (tests) WHARF_BLOOM_SATURATE=1 sets every bit of the walk
-// kernels' source filters, so every position is a positive and the exact checks decide
-void walk_counters_reset(wharf_handle* h, hipStream_t s)
-{
-    HIPCHK(hipMemsetAsync(h->counters.p, 0, 24, s));
-    HIPCHK(hipMemsetAsync(h->counters.as<unsigned long long>() + 7, 0, 8, s));
-    const char* sat = getenv("WHARF_BLOOM_SATURATE");
-    if (sat && atoi(sat)) HIPCHK(hipMemsetAsync(h->bitmap.as<uint32_t>() + h->bitmap_words(), 0xFF, kFilterWords * 4, s));
-}
-
-// The plan of an update batch as soon as its sources' bitmap is final (do_update,
-// before the CSR kernels): the node2vec MH plan (rewalk points + the sorted re-walk
-// list, k_rewalk_plan_lean) or a scan-only update's rewalk-point scan.  Both read
-// the walk matrix and the bitmap / filters alone, which the CSR update does not
-// touch, so they run on s2 beside it (streaming reads against the CSR update's
-// latency-bound kernels); walk_update joins ev_plan before the re-walk.
-// WHARF_EARLY_PLAN=0 keeps them on s after the CSR update (A/B and tests).
-void early_plan(wharf_handle* h, uint64_t k, uint32_t flags)
-{
-    h->early_plan = false;
-    if (!h->has_walks || !h->W) return;
-    const char* ep = getenv("WHARF_EARLY_PLAN");
-    if (!(ep && *ep && atoi(ep) != 0)) return;   // (off until measured on the GPU)
-    WalkArgs a = h->walk_args();
-    plan_fields(h, k, flags, a);
-    if (!((a.model == kNode2Vec && !a.det) || a.scan_only)) return;
-    HIPCHK(hipStreamSynchronize(h->s2));   // (a batch that failed after its plan left it running)
-    walk_counters_reset(h, h->s2);
-    launch_walk(a, true, h->s2, kWalkPlanOnly);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(h->ev_plan, h->s2));
-    h->early_plan = true;
-}
-
 void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected_out, uint64_t* n_affected)
 {
     hipStream_t s = h->s;
-    const bool early = h->early_plan;
-    h->early_plan = false;
     if (h->has_walks && h->W) {
-        if (!early) walk_counters_reset(h, s);   // (the early plan reset them on s2 and counts in them)
+        HIPCHK(hipMemsetAsync(h->counters.p, 0, 24, s));
+        HIPCHK(hipMemsetAsync(h->counters.as<unsigned long long>() + 7, 0, 8, s));
         h->st_park_passes = 0;
+        // tests: WHARF_BLOOM_SATURATE=1 sets every bit of the walk kernels' source
+        // filters, so every position is a positive and the exact checks decide
+        const char* sat = getenv("WHARF_BLOOM_SATURATE");
+        if (sat && atoi(sat)) HIPCHK(hipMemsetAsync(h->bitmap.as<uint32_t>() + h->bitmap_words(), 0xFF, kFilterWords * 4, s));
         WalkArgs a = h->walk_args();
-        plan_fields(h, k, flags, a);
+        a.scan_only = (flags & WHARF_APPLY_WALK_UPDATES) ? 0 : 1;
+        // chunked scans: non-temporal row loads when most walks are expected to re-walk.  The
+        // share grows with k * L / n (RMAT batches: configs[2] 0.19 -> 81 % re-walk, NT loads
+        // win; configs[3] 1/8 shard 0.024 -> 32 %, they lose 35 %); WHARF_NT_ROWS=0/1 forces it
+        const char* ntr = getenv("WHARF_NT_ROWS");
+        a.nt_rows = ntr ? (atoi(ntr) != 0) : ((double)k * h->L >= 0.08 * (double)std::max<uint64_t>(h->n, 1));
         // deterministic mode: suffixes walked once per (round, batch source) and copied
         // (k_det_suffix + k_rewalk_chunked<true>) while the table stays small; WHARF_NO_MEMO=1 (tests)
         // re-walks every suffix (k_rewalk_sweep)
@@ -834,7 +778,14 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
             a.memo_k = k;
             a.memo_stride = (uint32_t)stride4;
         }
-        if (a.model == kNode2Vec && !a.det) {
+        if (a.model == kNode2Vec && !a.det) {   // k_rewalk_plan's compacted, sorted re-walk list
+            h->defer.ensure(h->W * 8);
+            a.defer = h->defer.as<uint64_t>();
+            const char* rwm = getenv("WHARF_N2V_REWALK");   // =block: k_rewalk_block (row-staged stores)
+            if (rwm && std::string(rwm) == "block" && !a.scan_only) {
+                h->bdesc.ensure(((h->W + 255) / 256) * 8);
+                a.bdesc = h->bdesc.as<uint64_t>();
+            }
             const char* no_stab = getenv("WHARF_NO_START_TABLE");   // A/B and tests: binary search at every start
             if (!a.scan_only && k && !(no_stab && atoi(no_stab))) {
                 // start states (x, prev): x a batch source, prev an in-neighbour of it, so at most
@@ -879,8 +830,7 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         const char* rw = getenv("WHARF_N2V_REWALK");
         a.park = a.model == kNode2Vec && !a.det && a.anchor && !a.scan_only && rw && std::string(rw) == "park";
         h->walks_changed();
-        if (early) HIPCHK(hipStreamWaitEvent(s, h->ev_plan, 0));
-        launch_walk(a, true, s, early ? kWalkAfterPlan : kWalkAll);
+        launch_walk(a, true, s);
         HIPCHK(hipGetLastError());
         if (a.park) park_passes(h, a);
         HIPCHK(hipEventRecord(h->ev[3], s));
@@ -1030,8 +980,6 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         }
         h->epoch = epoch;
         h->dead_slots += dead;
-        // the sources' bitmap is final: the node2vec plan / a scan-only update's scan starts on s2
-        early_plan(h, k, flags);
         h->grown = grow;
         h->scratch.ensure(std::max<uint64_t>(saved, 1) * 4);
         h->start_bound = saved + (insert ? total_chg : 0);   // the sources' degrees after the update, at most

@@ -77,10 +77,7 @@ struct RowPlan {
 unsigned grid_for(uint64_t work, unsigned block);
 unsigned cu_count();
 
-// part (re-walks): kWalkAll, or the split the host overlaps with the CSR update: kWalkPlanOnly (the
-// node2vec plan, or the whole rewalk-point scan when a.scan_only) and kWalkAfterPlan (the rest)
-enum { kWalkAll = 0, kWalkPlanOnly = 1, kWalkAfterPlan = 2 };
-void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s, int part = kWalkAll);
+void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s);
 // node2vec MH re-walk passes: fresh = the input is k_rewalk_plan's list, park = walkers that need
 // an uncached anchor are appended to `out` instead of initialising it in the wave
 void launch_rewalk_park(const WalkArgs& a, int fresh, int park, const void* in, const unsigned long long* in_cnt,

@@ -11,7 +11,6 @@
 //   ehash          node2vec: edge set for has_edge (32-B buckets)
 //   bitmap[n/32]   batch-source set for the rewalk-point scan, + its Bloom filter
 #include <cstdlib>
-#include <stdexcept>
 #include <string>
 #include <type_traits>
 
@@ -1919,11 +1918,9 @@ static bool flat_list()
     return e && std::string(e) == "flat";
 }
 
-void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s, int part)
+void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
 {
     if (a.W == 0) return;
-    if (part != kWalkAll && !(rewalk && ((a.model == kNode2Vec && !a.det) || a.scan_only)))
-        throw std::runtime_error("launch_walk: only the node2vec plan or a scan-only update splits");
     // re-walks: persistent blocks (8 per CU, 16 KiB of Bloom filter each), so
     // the filter is copied to LDS once per block, not once per 256 walks
     const dim3 grid(rewalk ? std::min<uint64_t>((a.W + 255) / 256, (uint64_t)cu_count() * 8) : walk_grid(a.W)),
@@ -1936,14 +1933,13 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s, int part)
 #define WHARF_LAUNCH(M, D)                                                                   \
     do {                                                                                     \
         if (rewalk && M == kNode2Vec) {                                                      \
-            if (part == kWalkAfterPlan) {                                                    \
-            } else if (plan_lean) {                                                          \
+            if (plan_lean) {                                                                 \
                 if (a.nt_rows) hipLaunchKernelGGL(k_rewalk_plan_lean<true>, pgrid, dim3(1024), 0, s, a); \
                 else hipLaunchKernelGGL(k_rewalk_plan_lean<false>, pgrid, dim3(1024), 0, s, a);  \
             } else {                                                                         \
                 hipLaunchKernelGGL(k_rewalk_plan, grid, block, 0, s, a);                     \
             }                                                                                \
-            if (!a.scan_only && !a.park && part != kWalkPlanOnly) { /* park: the host runs the passes */ \
+            if (!a.scan_only && !a.park) { /* park: the host runs the passes */              \
                 if (a.bdesc) hipLaunchKernelGGL((k_rewalk_block<M>), lgrid, block, 0, s, a);     \
                 else if (flat_list()) hipLaunchKernelGGL((k_rewalk_list<M, D>), lgrid, block, 0, s, a); \
                 else hipLaunchKernelGGL((k_rewalk_sorted<M, D>), lgrid, block, 0, s, a);     \
@@ -1975,7 +1971,6 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s, int part)
         }
         return;
     }
-    if (rewalk && a.scan_only && part == kWalkAfterPlan) return;   // the scan ran as the plan
     if (rewalk && a.scan_only && chunked) {
         // WHARF_SCAN_KERNEL (A/B and tests): lean (default) = k_rewalk_scan_lean, 64-KiB
         // filter, where 7 * 4 * W fits 32 bits; big = k_rewalk_scan_big (round 2, also lean's

@@ -414,8 +414,6 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     # node2vec WEIGHT inits of the re-walk: return-first (default: a step settled by any non-return
     # anchor reads only its proposals' targets) or always the full init
     monkeypatch.setenv("WHARF_RET_FIRST", "0" if path in ("sorted/plain-rows", "flat/slack-repack") else "1")
-    # node2vec plan / scan-only rewalk points on a second stream beside the CSR update (default) or after it
-    monkeypatch.setenv("WHARF_EARLY_PLAN", "0" if path in ("sorted/slack", "flat/move") else "1")
     # node2vec plan (rewalk points + the binned re-walk list): on the lean scan (default) or k_rewalk_plan
     monkeypatch.setenv("WHARF_PLAN_KERNEL", "chunked" if path in ("flat/move", "sorted/plain-rows", "park/repack-tail")
                        else "lean")
