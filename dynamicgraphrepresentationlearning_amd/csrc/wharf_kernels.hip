@@ -1550,7 +1550,7 @@ __device__ __forceinline__ uint64_t wave_sort_entries(uint64_t ent)
 
 // (105 VGPRs, 4 waves/SIMD; forcing 5 spills 12 B and measured no faster:
 // configs[2] node2vec batch 65.4 vs 63.6 ms)
-template <int MODEL, bool DET>
+template <int MODEL, bool DET, bool RF = false>   // RF: return-first inits (WalkArgs::ret_first, A/B)
 __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
 {
     uint32_t steps = 0, accepts = 0, inits = 0;
@@ -1591,7 +1591,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
         for (uint32_t pos = first; pos < L; pos++) {
             uint32_t val = kSent;
             if (active && pos > p && w.rc.deg) {
-                val = walk_step<MODEL, DET, false, true>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
+                val = walk_step<MODEL, DET, false, RF>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
                 steps++;
             }
             // the lanes are walks scattered over a block (sorted by rewalk point),
@@ -1669,7 +1669,7 @@ __global__ __launch_bounds__(256) void k_rewalk_block(WalkArgs a)
                 if (active && pos > p) {
                     uint32_t val = kSent;
                     if (w.rc.deg) {
-                        val = walk_step<MODEL, false, false, true>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, inits);
+                        val = walk_step<MODEL, false>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, inits);
                         steps++;
                     }
                     tile[j][li - base] = val;
@@ -1735,7 +1735,7 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
         if (pos < L) {
             uint32_t val = kSent;
             if (w.rc.deg) {
-                val = walk_step<MODEL, DET, false, true>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
+                val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
                 steps++;
             }
             walks[(uint64_t)pos * W + li] = val;
@@ -1821,7 +1821,7 @@ __global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* 
         if (has) {
             uint32_t val = kSent;
             const bool live = w.rc.deg != 0;   // a walk at a vertex without out-edges ends
-            if (live) val = walk_step<MODEL, false, PARK, !PARK>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, inits, &park);
+            if (live) val = walk_step<MODEL, false, PARK>(a, w, nullptr, pos - 1, wlo, whi, ep, accepts, inits, &park);
             if (!park) {
                 steps += live;
                 walks[(uint64_t)pos * W + li] = val;
@@ -1942,6 +1942,7 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
             if (!a.scan_only && !a.park) { /* park: the host runs the passes */              \
                 if (a.bdesc) hipLaunchKernelGGL((k_rewalk_block<M>), lgrid, block, 0, s, a);     \
                 else if (flat_list()) hipLaunchKernelGGL((k_rewalk_list<M, D>), lgrid, block, 0, s, a); \
+                else if (a.ret_first) hipLaunchKernelGGL((k_rewalk_sorted<M, D, M == kNode2Vec>), lgrid, block, 0, s, a); \
                 else hipLaunchKernelGGL((k_rewalk_sorted<M, D>), lgrid, block, 0, s, a);     \
             }                                                                                \
         } else if (rewalk) {                                                                 \
