@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--shard", type=int, default=1,
                     help="keep only rank 0's walk shard of an N-way split (the per-GPU work of an N-GPU run; "
                          "the CSR stays whole, as on every rank)")
+    ap.add_argument("--shard-index", type=int, default=0, help="which rank's shard of the --shard split to keep")
     a = ap.parse_args()
     import torch
     import dynamicgraphrepresentationlearning_amd as W
@@ -61,9 +62,9 @@ def main():
     deg = np.diff(off.astype(np.int64))
     if a.shard > 1:
         from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards
-        lo, hi = balanced_shards(deg, a.shard)[0]
+        lo, hi = balanced_shards(deg, a.shard)[a.shard_index]
         g.set_shard(lo, hi)
-        print(f"shard 0 of {a.shard}: start vertices [{lo}, {hi}), {g.number_of_walks} walks", flush=True)
+        print(f"shard {a.shard_index} of {a.shard}: start vertices [{lo}, {hi}), {g.number_of_walks} walks", flush=True)
     g.generate_initial_random_walks()
     first_ms, first_inits = g.stats()["last_walk_kernel_ms"], g.stats()["last_anchor_inits"]
     g.generate_initial_random_walks()
@@ -136,7 +137,7 @@ def main():
     res = {"config": f"RMAT scale {a.scale}, {a.samples} undirected samples (seed 4), {a.model} {'deterministic' if a.det else 'MH'}, wpv {a.wpv}, "
                      f"L 80, {a.batches} {'insert+delete' if a.mixed else 'insert'} batches of "
                      "generate_batch_of_edges(5000, n, b, false, false)",
-           "n": n, "m": m, "walks": g.number_of_walks, "shard_of": a.shard, "build_s": round(t_build, 1),
+           "n": n, "m": m, "walks": g.number_of_walks, "shard_of": a.shard, "shard_index": a.shard_index, "build_s": round(t_build, 1),
            "gen_ms": round(st["last_walk_kernel_ms"], 2), "gen_Gsteps_per_s": round(gen_rate, 2),
            "first_gen_ms": round(first_ms, 2), "first_gen_anchor_inits": first_inits,
            "steps_ok": ok_steps, "bad_transitions": bad, "oracle_window_identical": same,
