@@ -105,6 +105,8 @@ struct wharf_handle {
     DevBuf tmp, k1, k2, flags, chg, cf, runstart, runs, count, pairs, sel, defer, rplan, pscan, scratch;
     DevBuf preoff;                             // node2vec MH: per-source degree prefix of the anchor pre-init
     DevBuf stab;                               // node2vec MH re-walk: start-state anchor table (k_rewalk_sorted)
+    DevBuf sanc;                               // anchor carry: the sources' old anchor entries (k_save_rows)
+    bool symmetric = false;                    // every edge's reverse is an edge (anchor carry needs it)
     DevBuf park, parkc;                        // node2vec MH re-walk passes: two parked-walker lists, their counts
     DevBuf bdesc;                              // node2vec MH block re-walk: per 256-walk block, its run of the list
     uint32_t st_park_passes = 0;               // passes of the last re-walk by passes (0: lock-step kernel)
@@ -656,7 +658,7 @@ void free_handle(wharf_handle* h)
                       &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->walks, &h->aff, &h->rtab,
                       &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags, &h->chg, &h->cf,
                       &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel, &h->defer, &h->rplan, &h->pscan,
-                      &h->scratch, &h->stab, &h->preoff, &h->park, &h->parkc, &h->bdesc})
+                      &h->scratch, &h->stab, &h->preoff, &h->park, &h->parkc, &h->bdesc, &h->sanc})
         b->release();
     h->free_snaps();
     for (auto& e : h->ev)
@@ -666,9 +668,19 @@ void free_handle(wharf_handle* h)
 }
 
 // keys in h->k1 (cnt of them) -> canonical CSR
-void build_graph_from_keys(wharf_handle* h, uint64_t cnt, bool drop_loops)
+void build_graph_from_keys(wharf_handle* h, uint64_t cnt, bool drop_loops, bool symmetric_by_construction)
 {
     const uint64_t mm = h->unique_keys(cnt, drop_loops, 32 + std::max<uint32_t>(bits_for(h->n), 1));
+    h->symmetric = symmetric_by_construction;
+    if (!symmetric_by_construction && h->anchors) {   // (only node2vec MH's anchor carry asks)
+        unsigned long long* asym = h->errflag.as<unsigned long long>() + 3;
+        HIPCHK(hipMemsetAsync(asym, 0, 8, h->s));
+        launch_keys_symmetric(h->k1.as<uint64_t>(), mm, asym, h->s);
+        unsigned long long v = 1;
+        HIPCHK(hipMemcpyAsync(&v, asym, 8, hipMemcpyDeviceToHost, h->s));
+        h->sync();
+        h->symmetric = v == 0;
+    }
     h->csr_from_keys(mm);
     // the keys and sort temporaries are done with: free them before the records
     // (configs[4]: 2 x 29 GB of keys next to 131 GB of 32-B records)
@@ -927,8 +939,15 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         }
         uint64_t k = 0;
         uint32_t total_chg = 0;
+        unsigned long long batch_asym = 0;
         HIPCHK(hipMemcpyAsync(&k, h->count.p, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(&total_chg, h->cf.as<uint32_t>() + mb, 4, hipMemcpyDeviceToHost, s));
+        if (h->anchors && h->symmetric) {   // a batch without every reverse edge leaves the graph directed
+            unsigned long long* asym = h->errflag.as<unsigned long long>() + 3;
+            HIPCHK(hipMemsetAsync(asym, 0, 8, s));
+            launch_keys_symmetric(bkeys, mb, asym, s);
+            HIPCHK(hipMemcpyAsync(&batch_asym, asym, 8, hipMemcpyDeviceToHost, s));
+        }
         h->sync();
 
         // 4. the batch sources' rows (wharfmh.h:504-540, 652-690): merged in place
@@ -980,14 +999,23 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         }
         h->epoch = epoch;
         h->dead_slots += dead;
+        if (batch_asym) h->symmetric = false;
+        // Anchor carry (node2vec MH on an undirected graph): the entries of the sources' rows travel
+        // through the merge and only those whose anchor can change are reset (k_anchor_invalidate);
+        // otherwise every entry of a rebuilt row starts empty.  WHARF_ANCHOR_CARRY=0 (A/B, tests).
+        const char* acv = getenv("WHARF_ANCHOR_CARRY");
+        const bool carry = h->anchors && h->symmetric && !(acv && *acv && atoi(acv) == 0);
+        uint64_t* anc_base = h->anchors ? h->erec.as<uint64_t>() + 2 : nullptr;
+        if (carry) h->sanc.ensure(std::max<uint64_t>(saved, 1) * 8);
         h->grown = grow;
         h->scratch.ensure(std::max<uint64_t>(saved, 1) * 4);
         h->start_bound = saved + (insert ? total_chg : 0);   // the sources' degrees after the update, at most
         const uint32_t rs = (uint32_t)h->rec_stride();
-        launch_save_rows(h->runs.as<RunInfo>(), k, h->adj.as<uint32_t>(), sofs, h->scratch.as<uint32_t>(), s);
+        launch_save_rows(h->runs.as<RunInfo>(), k, h->adj.as<uint32_t>(), sofs, h->scratch.as<uint32_t>(), anc_base,
+                         carry ? h->sanc.as<uint64_t>() : nullptr, s);
         launch_merge_rows(h->runs.as<RunInfo>(), k, bkeys, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(),
                           h->scratch.as<uint32_t>(), sofs, relofs, h->pool_used, insert, h->rplan.as<RowPlan>(),
-                          h->adj.as<uint32_t>(), s);
+                          h->adj.as<uint32_t>(), carry ? h->sanc.as<uint64_t>() : nullptr, anc_base, s);
         launch_commit_rows(h->runs.as<RunInfo>(), k, h->rplan.as<RowPlan>(), h->epoch, h->off.as<uint64_t>(),
                            h->deg.as<uint32_t>(), h->cap.as<uint32_t>(), h->vrec.as<ERec>(), h->row_epoch.as<uint32_t>(), s);
         h->pool_used += grow;
@@ -995,7 +1023,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         // records: the source rows' slots (anchors reset), then every slot whose
         // target is a source (one streaming scan of the pool)
         launch_erec_rows(h->runs.as<RunInfo>(), k, h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->adj.as<uint32_t>(),
-                         h->vrec.as<ERec>(), h->erec.as<ERec>(), rs, s);
+                         h->vrec.as<ERec>(), h->erec.as<ERec>(), rs, carry ? 1 : 0, s);
         HIPCHK(hipEventRecord(h->ev[4], s));
         launch_patch_in_edges(h->adj.as<uint32_t>(), h->pool_used, h->bitmap.as<uint32_t>(),
                               h->bitmap.as<uint32_t>() + h->bitmap_words(), h->vrec.as<ERec>(), h->erec.as<ERec>(), rs, s);
@@ -1012,6 +1040,11 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
                 if (insert) h->ehash_used += total_chg;
             }
             h->update_filters(h->runs.as<RunInfo>(), k);
+            // anchor carry: reset the carried entries a changed edge can affect (c's filter, new rows)
+            if (carry)
+                launch_anchor_invalidate(bkeys, mb, h->chg.as<uint32_t>(), h->off.as<uint64_t>(), h->deg.as<uint32_t>(),
+                                         h->adj.as<uint32_t>(), anc_base, h->fpool.p ? h->fdir.as<uint64_t>() : nullptr,
+                                         h->fpool.p ? h->fpool.as<uint32_t>() : nullptr, s);
         }
         HIPCHK(hipGetLastError());   // a failed launch of the CSR pipeline surfaces here
         HIPCHK(hipEventRecord(h->ev[1], s));
@@ -1079,7 +1112,7 @@ int wharf_create(const wharf_config* cfg, uint64_t n, uint64_t m, const uint64_t
         HIPCHK(hipMemcpyAsync(&errv, h->errflag.p, 8, hipMemcpyDeviceToHost, h->s));
         h->sync();
         REQUIRE(errv == 0, WHARF_E_INVALID, "edge target >= n");
-        build_graph_from_keys(h, m, false);
+        build_graph_from_keys(h, m, false, false);
         h->k1.release();
         h->k2.release();
         h->off2.release();
@@ -1110,7 +1143,7 @@ int wharf_create_rmat(const wharf_config* cfg, uint64_t n, uint64_t edges_number
         REQUIRE((1ull << (bits_for(vertices_number) - 1)) <= n, WHARF_E_INVALID, "n smaller than the RMAT vertex range");
         h = new_handle(cfg, n, device);
         rmat_keys(h, edges_number, vertices_number, seed, /*directed=*/0, a, b, c);
-        build_graph_from_keys(h, 2 * edges_number, /*drop self loops*/ true);
+        build_graph_from_keys(h, 2 * edges_number, /*drop self loops*/ true, /*symmetric: undirected samples*/ true);
         h->k1.release();
         h->k2.release();
         h->tmp.release();

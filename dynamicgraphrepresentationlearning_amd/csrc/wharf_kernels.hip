@@ -601,8 +601,12 @@ __global__ __launch_bounds__(256) void k_anchor_preinit(WalkArgs a, const uint64
         const uint32_t y = a.adj[e];
         const Row ry = load_rec(a.vrec, y);
         uint32_t an = 0, cls = 0;
-        // (y, x): entry of slot x -> y (a walker that crosses it and stays at y needs y's row)
-        const bool need_a = ry.deg != 0;
+        // (y, x): entry of slot x -> y (a walker that crosses it and stays at y needs y's row);
+        // an entry carried through the batch (anchor carry) is still valid
+        const uint64_t ca = a.anchor[e * kAnchorStride];
+        const bool carried = ca != kAnchorNone64 && ((uint32_t)(ca >> 32) & 0x3FFFFFFFu) >= ry.epoch &&
+                             (uint32_t)(ca >> 62) != kClassNoReturn;
+        const bool need_a = ry.deg != 0 && !carried;
         anchor_compute(a, need_a, ry, rx, an, cls, inits);
         if (need_a) a.anchor[e * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
         // (x, y): entry of slot y -> x, and the start-state table
@@ -2410,13 +2414,18 @@ __global__ void k_plan_rows(const RunInfo* __restrict__ runs, uint64_t k, const 
     }
 }
 
-// block per run: the old row, copied aside (the merge may overwrite it in place)
+// block per run: the old row, copied aside (the merge may overwrite it in place);
+// with sanc, its anchor entries too (anchor carry, k_anchor_invalidate)
 __global__ void k_save_rows(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ adj,
-                            const uint64_t* __restrict__ sofs, uint32_t* __restrict__ scratch)
+                            const uint64_t* __restrict__ sofs, uint32_t* __restrict__ scratch,
+                            const uint64_t* __restrict__ anc, uint64_t* __restrict__ sanc)
 {
     const RunInfo ri = runs[blockIdx.x];
     uint32_t* __restrict__ out = scratch + sofs[blockIdx.x];
-    for (uint64_t i = threadIdx.x; i < ri.end - ri.off; i += blockDim.x) out[i] = adj[ri.off + i];
+    for (uint64_t i = threadIdx.x; i < ri.end - ri.off; i += blockDim.x) {
+        out[i] = adj[ri.off + i];
+        if (sanc) sanc[sofs[blockIdx.x] + i] = anc[(ri.off + i) * kAnchorStride];
+    }
 }
 
 // first index in a[0, n) with a[i] >= x (ascending u32)
@@ -2450,7 +2459,8 @@ __global__ void k_merge_rows(const RunInfo* __restrict__ runs, const uint64_t* _
                              const uint32_t* __restrict__ chg, const uint32_t* __restrict__ cf,
                              const uint32_t* __restrict__ scratch, const uint64_t* __restrict__ sofs,
                              const uint64_t* __restrict__ relofs, uint64_t pool_end, int insert,
-                             RowPlan* __restrict__ plan, uint32_t* __restrict__ adj)
+                             RowPlan* __restrict__ plan, uint32_t* __restrict__ adj,
+                             const uint64_t* __restrict__ sanc, uint64_t* __restrict__ anc)
 {
     const uint64_t j = blockIdx.x;
     const RunInfo ri = runs[j];
@@ -2464,17 +2474,21 @@ __global__ void k_merge_rows(const RunInfo* __restrict__ runs, const uint64_t* _
         const uint32_t x = old[i];
         const uint32_t lb = lower_bound_dst(bk, nb, x);
         const uint32_t below = cf[ri.rs + lb] - base;
-        if (insert) {
-            adj[noff + i + below] = x;
-        } else if (!(lb < nb && (uint32_t)bk[lb] == x && chg[ri.rs + lb])) {
-            adj[noff + i - below] = x;
+        uint64_t at = ~0ull;
+        if (insert) at = noff + i + below;
+        else if (!(lb < nb && (uint32_t)bk[lb] == x && chg[ri.rs + lb])) at = noff + i - below;
+        if (at != ~0ull) {
+            adj[at] = x;
+            if (sanc) anc[at * kAnchorStride] = sanc[sofs[j] + i];   // the entry travels with its edge
         }
     }
     if (insert) {
         for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x) {
             if (!chg[ri.rs + t]) continue;
             const uint32_t x = (uint32_t)bk[t];
-            adj[noff + (cf[ri.rs + t] - base) + lower_bound_u32(old, d, x)] = x;
+            const uint64_t at = noff + (cf[ri.rs + t] - base) + lower_bound_u32(old, d, x);
+            adj[at] = x;
+            if (sanc) anc[at * kAnchorStride] = kAnchorNone64;
         }
     }
     if (reloc) {
@@ -2510,13 +2524,74 @@ __global__ void k_commit_rows(const RunInfo* __restrict__ runs, uint64_t k, cons
 // source's row) start empty: see anchor_lookup and DESIGN.md §4
 __global__ void k_erec_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ off,
                             const uint32_t* __restrict__ deg, const uint32_t* __restrict__ adj,
-                            const ERec* __restrict__ vrec, ERec* __restrict__ erec, uint32_t rs)
+                            const ERec* __restrict__ vrec, ERec* __restrict__ erec, uint32_t rs, int keep_anc)
 {
     const uint32_t s = runs[blockIdx.x].src;
     const uint64_t b = off[s], e = b + deg[s];
     for (uint64_t j = b + threadIdx.x; j < e; j += blockDim.x) {
         erec[j * rs] = vrec[adj[j]];
-        if (rs == 2) reinterpret_cast<uint64_t*>(erec)[j * kAnchorStride + 2] = kAnchorNone64;
+        if (rs == 2 && !keep_anc) reinterpret_cast<uint64_t*>(erec)[j * kAnchorStride + 2] = kAnchorNone64;
+    }
+}
+
+// Anchor carry (node2vec MH, undirected graphs).  The entry of slot x -> y holds
+// the anchor of state (y, x): 21 proposals from y's row, classed by
+// has_edge(x, proposal).  A batch that changes x's row by the edges (x, c)
+// changes only the classes of proposals equal to some c, so the anchor can
+// differ only where c is in y's row: y in N(x) and N(c).  Those entries are
+// reset; every other entry of x's row is carried through the merge
+// (k_save_rows / k_merge_rows) and equals what a re-initialisation would give
+// (the anchor is a pure function of the two rows).  One wave per
+// changed batch edge.  With the neighbour filters (fdir / fpool, refilled for
+// the new rows), x's row is walked and each y tested against c's filter: one
+// independent load per element, and a false positive only resets an entry
+// that did not need it.  Without them the smaller row's elements are searched
+// in the larger row.
+__global__ __launch_bounds__(256) void k_anchor_invalidate(const uint64_t* __restrict__ bkeys, uint64_t mb,
+                                                           const uint32_t* __restrict__ chg,
+                                                           const uint64_t* __restrict__ off,
+                                                           const uint32_t* __restrict__ deg,
+                                                           const uint32_t* __restrict__ adj, uint64_t* __restrict__ anc,
+                                                           const uint64_t* __restrict__ fdir,
+                                                           const uint32_t* __restrict__ fpool)
+{
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t lane = __lane_id();
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < mb; i += nw) {
+        const uint64_t key = bkeys[i];
+        const uint32_t x = (uint32_t)(key >> 32), c = (uint32_t)key;
+        if (!chg[i] || x == c) continue;   // (wave-uniform)
+        const Row rx{x, deg[x], 0u, off[x]}, rcv{c, deg[c], 0u, off[c]};
+        if (fpool) {
+            const uint64_t fd = fdir[c];
+            for (uint32_t j = lane; j < rx.deg; j += 64) {
+                const uint64_t h = filt_hash(adj[rx.off + j]);
+                const uint32_t b = filt_bits(h);
+                if ((fpool[filt_word(fd, h)] & b) == b) anc[(rx.off + j) * kAnchorStride] = kAnchorNone64;
+            }
+        } else if (rx.deg <= rcv.deg) {
+            for (uint32_t j = lane; j < rx.deg; j += 64)
+                if (row_find(adj, rcv, adj[rx.off + j]) >= 0) anc[(rx.off + j) * kAnchorStride] = kAnchorNone64;
+        } else {
+            for (uint32_t j = lane; j < rcv.deg; j += 64) {
+                const int64_t e = row_find(adj, rx, adj[rcv.off + j]);
+                if (e >= 0) anc[(uint64_t)e * kAnchorStride] = kAnchorNone64;
+            }
+        }
+    }
+}
+
+// keys sorted ascending: any key whose reverse (v, u) is missing sets *asym
+__global__ void k_keys_symmetric(const uint64_t* __restrict__ keys, uint64_t m, unsigned long long* __restrict__ asym)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i], r = (k << 32) | (k >> 32);
+        uint64_t lo = 0, hi = m;
+        while (lo < hi) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            if (keys[mid] < r) lo = mid + 1; else hi = mid;
+        }
+        if (lo >= m || keys[lo] != r) *asym = 1ull;   // (a plain store: every writer writes 1)
     }
 }
 
@@ -2931,21 +3006,30 @@ void launch_compact_put(const uint32_t* sadj, const uint64_t* sanc, uint64_t cnt
 void launch_scatter_offsets(const uint32_t* order, const uint64_t* snoff, uint64_t n, uint64_t* off, hipStream_t s)
 { hipLaunchKernelGGL(k_scatter_offsets, grid_for(n + 1, 256), 256, 0, s, order, snoff, n, off); }
 void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* adj, const uint64_t* sofs, uint32_t* scratch,
-                      hipStream_t s)
-{ if (k) hipLaunchKernelGGL(k_save_rows, (unsigned)k, 256, 0, s, runs, adj, sofs, scratch); }
+                      const uint64_t* anc, uint64_t* sanc, hipStream_t s)
+{ if (k) hipLaunchKernelGGL(k_save_rows, (unsigned)k, 256, 0, s, runs, adj, sofs, scratch, anc, sanc); }
 void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint64_t* bkeys, const uint32_t* chg, const uint32_t* cf,
                        const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs, uint64_t pool_end,
-                       int insert, RowPlan* plan, uint32_t* adj, hipStream_t s)
+                       int insert, RowPlan* plan, uint32_t* adj, const uint64_t* sanc, uint64_t* anc, hipStream_t s)
 {
     if (k) hipLaunchKernelGGL(k_merge_rows, (unsigned)k, 256, 0, s, runs, bkeys, chg, cf, scratch, sofs, relofs,
-                              pool_end, insert, plan, adj);
+                              pool_end, insert, plan, adj, sanc, anc);
 }
+void launch_anchor_invalidate(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint64_t* off,
+                              const uint32_t* deg, const uint32_t* adj, uint64_t* anc, const uint64_t* fdir,
+                              const uint32_t* fpool, hipStream_t s)
+{
+    if (mb) hipLaunchKernelGGL(k_anchor_invalidate, (unsigned)std::min<uint64_t>((mb + 3) / 4, (uint64_t)cu_count() * 8),
+                               256, 0, s, bkeys, mb, chg, off, deg, adj, anc, fdir, fpool);
+}
+void launch_keys_symmetric(const uint64_t* keys, uint64_t m, unsigned long long* asym, hipStream_t s)
+{ if (m) hipLaunchKernelGGL(k_keys_symmetric, grid_for(m, 256), 256, 0, s, keys, m, asym); }
 void launch_commit_rows(const RunInfo* runs, uint64_t k, const RowPlan* plan, uint32_t epoch, uint64_t* off,
                         uint32_t* deg, uint32_t* cap, ERec* vrec, uint32_t* row_epoch, hipStream_t s)
 { if (k) hipLaunchKernelGGL(k_commit_rows, grid_for(k, 256), 256, 0, s, runs, k, plan, epoch, off, deg, cap, vrec, row_epoch); }
 void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* off, const uint32_t* deg, const uint32_t* adj,
-                      const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s)
-{ if (k) hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, off, deg, adj, vrec, erec, rs); }
+                      const ERec* vrec, ERec* erec, uint32_t rs, int keep_anc, hipStream_t s)
+{ if (k) hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, off, deg, adj, vrec, erec, rs, keep_anc); }
 void launch_patch_in_edges(const uint32_t* adj, uint64_t slots, const uint32_t* bitmap, const uint32_t* bloom,
                            const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s)
 {

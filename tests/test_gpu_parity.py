@@ -414,6 +414,9 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     # node2vec WEIGHT inits of the re-walk: return-first (default: a step settled by any non-return
     # anchor reads only its proposals' targets) or always the full init
     monkeypatch.setenv("WHARF_RET_FIRST", "0" if path in ("sorted/plain-rows", "flat/slack-repack") else "1")
+    # node2vec anchor entries of the sources' rows carried through the merge, the ones a changed edge can
+    # affect reset (default, undirected graphs; the last, directed batch turns it off), or all reset
+    monkeypatch.setenv("WHARF_ANCHOR_CARRY", "0" if path in ("flat/move", "block/move-lazy") else "1")
     # node2vec plan (rewalk points + the binned re-walk list): on the lean scan (default) or k_rewalk_plan
     monkeypatch.setenv("WHARF_PLAN_KERNEL", "chunked" if path in ("flat/move", "sorted/plain-rows", "park/repack-tail")
                        else "lean")
