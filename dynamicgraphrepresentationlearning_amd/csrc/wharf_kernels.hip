@@ -2563,11 +2563,18 @@ __global__ __launch_bounds__(256) void k_anchor_invalidate(const uint64_t* __res
         if (!chg[i] || x == c) continue;   // (wave-uniform)
         const Row rx{x, deg[x], 0u, off[x]}, rcv{c, deg[c], 0u, off[c]};
         if (fpool) {
-            const uint64_t fd = fdir[c];
-            for (uint32_t j = lane; j < rx.deg; j += 64) {
-                const uint64_t h = filt_hash(adj[rx.off + j]);
+            // the smaller row's elements against the other row's filter; a positive found in c's
+            // row is located in x's row by a search (positives are few: N(x) and N(c) rarely meet)
+            const bool walk_x = rx.deg <= rcv.deg;
+            const Row& rw = walk_x ? rx : rcv;
+            const uint64_t fd = fdir[walk_x ? c : x];
+            for (uint32_t j = lane; j < rw.deg; j += 64) {
+                const uint32_t y = adj[rw.off + j];
+                const uint64_t h = filt_hash(y);
                 const uint32_t b = filt_bits(h);
-                if ((fpool[filt_word(fd, h)] & b) == b) anc[(rx.off + j) * kAnchorStride] = kAnchorNone64;
+                if ((fpool[filt_word(fd, h)] & b) != b) continue;
+                const int64_t e = walk_x ? (int64_t)(rx.off + j) : row_find(adj, rx, y);
+                if (e >= 0) anc[(uint64_t)e * kAnchorStride] = kAnchorNone64;
             }
         } else if (rx.deg <= rcv.deg) {
             for (uint32_t j = lane; j < rx.deg; j += 64)
