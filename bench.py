@@ -87,6 +87,18 @@ def parse():
     p.add_argument("--per-gpu-of-8", type=int, default=1,
                    help="configs[3] / configs[4]: the per-GPU work of their 8-GPU runs on this GPU (0 = off)")
     p.add_argument("--per8-batches", type=int, default=5, help="update batches per per_gpu_of_8 case")
+    p.add_argument("--jobs", default="configs3,configs4",
+                   help="at N > 1: BASELINE's 8-GPU jobs run on the ranks of this run (comma list; '' = none)")
+    p.add_argument("--job-batches", type=int, default=5, help="update batches per job (configs[4]: insert+delete pairs)")
+    p.add_argument("--job-scale-delta", type=int, default=0,
+                   help="rehearsals: RMAT scale of the jobs shifted by this (samples scaled alike), e.g. -4")
+    p.add_argument("--job-gather", type=int, default=1, help="time the jobs' bounded corpus all-gatherv (0 = off)")
+    p.add_argument("--job-one-gpu", type=int, default=1,
+                   help="configs[3] job: rank 0 also runs every walk on its GPU (the 1-GPU time) (0 = off)")
+    p.add_argument("--gather-chunk-bytes", type=int, default=4 << 30,
+                   help="device buffer of the bounded corpus gather (all ranks' rows of one chunk)")
+    p.add_argument("--gather-check", type=int, default=1,
+                   help="second gather pass checking the checksum of checksums (0 = off)")
     return p.parse_args()
 
 
@@ -550,6 +562,238 @@ def per_gpu_of_8(args, W, torch, dev, barrier):
     return out
 
 
+def _max_over_ranks(torch, dist, comm_dev, vals):
+    t = torch.tensor(list(vals), dtype=torch.float64, device=comm_dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
+
+
+def _sum_over_ranks(torch, dist, comm_dev, vals):
+    t = torch.tensor(list(vals), dtype=torch.float64, device=comm_dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.tolist()
+
+
+def _per_rank(torch, dist, comm_dev, vals, world):
+    """[world][len(vals)]: every rank's values (all-gathered)."""
+    t = torch.tensor(list(vals), dtype=torch.float64, device=comm_dev)
+    if not dist:
+        return [t.tolist()]
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev, world, rank, barrier, budget_bytes):
+    """The corpus reassembled for the downstream consumer (yskip,
+    vertex-classification.cpp:142-158) by the bounded full-mesh all-gatherv
+    (distributed.gather_corpus_chunked): chunks of at most `budget_bytes` land
+    in one reused buffer, local rows are read from the handle per chunk.  Timed
+    pass (the chunk is dropped), then a checked pass: the checksum of everything
+    every rank received equals the sum of the ranks' local checksums."""
+    from dynamicgraphrepresentationlearning_amd.distributed import corpus_checksum, gather_corpus_chunked, \
+        local_corpus_checksum
+    lo, hi = shards[rank]
+    on_dev = comm_dev != "cpu"
+    K = max(1, int(budget_bytes // (world * L * 4)))
+    stage = None if on_dev else torch.empty((K, L), dtype=torch.int32, device=f"cuda:{dev}")
+
+    def read_local(first, count, out):
+        if on_dev:
+            g.export_walk_rows(first, count, out)
+        else:   # gloo rehearsal: rows staged through the device buffer to host memory
+            g.export_walk_rows(first, count, stage[:count])
+            out.copy_(stage[:count].cpu())
+
+    barrier()
+    t1 = time.perf_counter()
+    st = gather_corpus_chunked(read_local, shards, n, wpv, L, K, None, device=comm_dev)
+    barrier()
+    ms = (time.perf_counter() - t1) * 1e3
+    ms_all = _max_over_ranks(torch, dist, comm_dev, [ms])[0]
+    rec = {"pattern": "gather_corpus_chunked: full-mesh batch_isend_irecv per chunk of local rows",
+           "backend": "nccl (RCCL over xGMI)" if on_dev else "gloo (host staging)",
+           "walks": sum(h_ - l_ for l_, h_ in shards) * wpv, "corpus_bytes": sum(h_ - l_ for l_, h_ in shards) * wpv * L * 4,
+           "rows_per_rank_per_chunk": K,
+           "buffer_bytes": K * world * L * 4, "chunks": st["chunks"], "ms": round(ms_all, 2),
+           "bytes_received_rank0": int(st["bytes_received"]),
+           "GBps_received_per_rank": round(st["bytes_received"] / (ms_all * 1e-3) / 1e9, 1) if ms_all else None}
+    if args.gather_check:
+        acc = torch.zeros((), dtype=torch.int64, device=comm_dev)
+
+        def sink(chunk, segs):
+            for r0, c, g0 in segs:
+                acc.add_(corpus_checksum(chunk[r0:r0 + c], g0, L))
+
+        gather_corpus_chunked(read_local, shards, n, wpv, L, K, sink, device=comm_dev)
+        mine = local_corpus_checksum(read_local, lo, hi, n, wpv, L, K, device=comm_dev)
+        tot = mine.clone()
+        if dist:
+            dist.all_reduce(tot)
+        ok = torch.tensor([1 if int(acc.item()) == int(tot.item()) else 0], dtype=torch.int64, device=comm_dev)
+        if dist:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        rec["checksum_of_checksums_ok"] = bool(ok.item())
+    if on_dev:
+        torch.cuda.empty_cache()
+    return rec
+
+
+JOBS = {
+    # BASELINE configs[3]: twitter-2010-sized, initial walks + streaming inserts, walks sharded over the
+    # ranks (strong scaling of the one job), corpus all-gathered
+    "configs3": dict(scale=25, samples=1_200_000_000, model="deepwalk", mixed=False, split="ranks",
+                     desc="twitter-2010-sized RMAT, DeepWalk MH, walks_per_vertex=10, L=80, insert batches; "
+                          "the 335 M walks split over the ranks"),
+    # BASELINE configs[4]: friendster-sized, node2vec p=.5 q=2 MH, mixed insert/delete; 656 M walks need
+    # 8 GPUs (253 GB per rank), so rank g runs shard g of 8 at every N (weak scaling: N/8 of the job)
+    "configs4": dict(scale=26, samples=1_800_000_000, model="node2vec", mixed=True, split="eighths",
+                     desc="friendster-sized RMAT, node2vec p=0.5 q=2 MH WEIGHT, walks_per_vertex=10, L=80, "
+                          "insert/delete pairs; rank g runs start-vertex shard g of 8"),
+}
+
+
+def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrier):
+    """One of BASELINE's 8-GPU jobs on the ranks of this run: the graph built on
+    every rank (replicated, wharfmh.h:275,761 shard by walk), the rank's walk
+    shard, first and warm generation, the bounded corpus all-gatherv, then
+    --job-batches update batches generate_batch_of_edges(5000, n, b, false,
+    undirected) (configs[4]: each inserted, then deleted,
+    throughput-latency.cpp:126,135).  Per update: barrier, the rank's wall time,
+    max over ranks.  configs[3] also runs, on rank 0 alone, every walk on one
+    GPU over the same graph: the 1-GPU time the job divides."""
+    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards
+    spec = JOBS[name]
+    scale = spec["scale"] + args.job_scale_delta
+    samples = spec["samples"] >> (-args.job_scale_delta) if args.job_scale_delta < 0 else spec["samples"]
+    n = 1 << scale
+    parts = world if spec["split"] == "ranks" else max(8, world)
+    node2vec = spec["model"] == "node2vec"
+    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, model=W.NODE2VEC if node2vec else W.DEEPWALK,
+                        paramP=0.5, paramQ=2.0, deterministic=False, seed=0x5EED)
+    g = None
+    try:
+        t0 = time.time()
+        g = W.WharfMH.from_rmat(n, samples, 2 * n, seed=4, config=cfg, device=dev)
+        deg = np.diff(g.offsets().astype(np.int64))
+        shards = balanced_shards(deg, parts)
+        lo, hi = shards[rank]
+        g.set_shard(lo, hi)
+        build_s = time.time() - t0
+        gen = []
+        for _ in range(2):   # first (node2vec: every anchor initialised) and warm generation
+            barrier()
+            t1 = time.perf_counter()
+            g.generate_initial_random_walks()
+            torch.cuda.synchronize(dev)
+            wall = (time.perf_counter() - t1) * 1e3
+            st = g.stats()
+            gen.append((wall, st["last_walk_kernel_ms"], st["steps"], st["last_anchor_inits"]))
+        gmax = _max_over_ranks(torch, dist, comm_dev, [gen[0][0], gen[1][0], gen[0][1], gen[1][1]])
+        gsum = _sum_over_ranks(torch, dist, comm_dev, [gen[1][2], gen[0][3]])
+        rec = {"workload": f"BASELINE {name}: {spec['desc']}; RMAT scale {scale}, {samples} undirected samples "
+                           f"(seed 4), m={g.number_of_edges()}",
+               "ranks": world, "walk_shards": parts,
+               "walks_this_run": int(sum(hi_ - lo_ for lo_, hi_ in shards[:world]) * 10),
+               "walks_whole_job": n * 10, "scaling": "strong (the job's walks split over the ranks)"
+               if spec["split"] == "ranks" else f"weak (rank g runs shard g of {parts}: {world}/{parts} of the job)",
+               "build_s_rank0": round(build_s, 1),
+               "first_generation_ms": round(gmax[0], 2), "generation_ms": round(gmax[1], 2),
+               "generation_kernel_ms_max": round(gmax[3], 2),
+               "generation_steps": int(gsum[0]),
+               "generation_walk_steps_per_s": round(gsum[0] / (gmax[1] * 1e-3), 1),
+               "first_generation_anchor_inits": int(gsum[1]),
+               "device_bytes_rank0": g.memory_footprint(verbose=False)["total_bytes"]}
+        if args.job_gather and world > 1:
+            free = torch.cuda.mem_get_info(dev)[0] if comm_dev != "cpu" else (8 << 30)
+            budget = max(64 << 20, min(args.gather_chunk_bytes, free // 4))
+            rec["corpus_allgatherv"] = corpus_gather_record(args, torch, dist, g, shards[:world], n, 10, 80, dev,
+                                                            comm_dev, world, rank, barrier, budget)
+        ids = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
+        per = {k: [] for k in ("wall", "graph", "walk", "in_edge", "steps", "affected", "inits")}
+        for b in range(args.job_batches):
+            batch = W.generate_batch_of_edges(5000, n, b, False, False, device=dev)
+            for ins in ((True, False) if spec["mixed"] else (True,)):
+                barrier()
+                t1 = time.perf_counter()
+                (g.insert_edges_batch if ins else g.delete_edges_batch)(batch, remove_dups=True, out=ids)
+                torch.cuda.synchronize(dev)
+                per["wall"].append((time.perf_counter() - t1) * 1e3)
+                st = g.stats()
+                per["graph"].append(st["last_graph_update_ms"])
+                per["walk"].append(st["last_walk_update_ms"])
+                per["in_edge"].append(st["last_csr_move_ms"])
+                per["steps"].append(st["steps"])
+                per["affected"].append(st["affected"])
+                per["inits"].append(st["last_anchor_inits"])
+        if per["wall"]:
+            job_ms = _max_over_ranks(torch, dist, comm_dev, per["wall"])
+            steps = _sum_over_ranks(torch, dist, comm_dev, per["steps"])
+            med = lambda k: float(np.median(per[k]))
+            ranks = _per_rank(torch, dist, comm_dev, [med("wall"), med("graph"), med("walk"), med("in_edge"),
+                                                     float(np.sum(per["steps"])), float(np.sum(per["walk"]))], world)
+            rec.update({
+                "updates": len(job_ms), "batch_median_ms": round(float(np.median(job_ms)), 3),
+                "batch_p90_ms": round(float(np.percentile(job_ms, 90)), 3),
+                "rewalk_walk_steps_per_update": int(np.mean(steps)),
+                "rewalk_walk_steps_per_s": round(float(np.sum(steps) / (np.sum(job_ms) * 1e-3)), 1),
+                "per_rank": {"batch_median_ms": [round(r[0], 3) for r in ranks],
+                             "graph_update_median_ms": [round(r[1], 3) for r in ranks],
+                             "walk_update_median_ms": [round(r[2], 3) for r in ranks],
+                             "in_edge_scan_median_ms": [round(r[3], 3) for r in ranks],
+                             "rewalk_Gsteps_per_s": [round(r[4] / r[5] / 1e6, 2) if r[5] else None for r in ranks]},
+                "rank_balance_max_over_min": round(max(r[0] for r in ranks) / max(min(r[0] for r in ranks), 1e-9), 3),
+                "mean_affected_walks_rank0": int(np.mean(per["affected"])),
+                "mean_anchor_inits_rank0": int(np.mean(per["inits"]))})
+        if spec["split"] == "ranks" and world > 1 and args.job_one_gpu:
+            # the same graph (after this job's batches) with every walk on rank 0's GPU
+            one = None
+            if rank == 0:
+                g.set_shard(0, n)
+                g.generate_initial_random_walks()
+                g.generate_initial_random_walks()
+                st = g.stats()
+                ids = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
+                o = _update_stream_from(g, W, n, args.job_batches, args.job_batches, spec["mixed"], ids, dev)
+                one = {"walks": g.number_of_walks, "generation_ms": round(st["last_walk_kernel_ms"], 2),
+                       "batch_median_ms": o["batch_median_ms"], "graph_update_median_ms": o["graph_update_median_ms"],
+                       "walk_update_median_ms": o["walk_update_median_ms"],
+                       "batches": f"generate_batch_of_edges(5000, n, b, false, undirected), "
+                                  f"b = {args.job_batches}..{2 * args.job_batches - 1}"}
+            barrier()
+            if one is not None:
+                rec["one_gpu_same_graph"] = one
+                if "batch_median_ms" in rec:
+                    rec["batch_ratio_one_gpu_to_job"] = round(one["batch_median_ms"] / rec["batch_median_ms"], 2)
+                rec["generation_ratio_one_gpu_to_job"] = round(one["generation_ms"] / rec["generation_kernel_ms_max"], 2)
+        return rec
+    except Exception as ex:   # noqa: BLE001 (a job that does not fit is reported, the headline still prints)
+        log(f"[rank {rank}] job {name} failed: {ex}")
+        return {"error": str(ex)[:500]}
+    finally:
+        if g is not None:
+            g.destroy()
+        torch.cuda.empty_cache()
+
+
+def _update_stream_from(g, W, n, first, batches, mixed, out, dev):
+    """_update_stream over batch seeds first .. first + batches - 1."""
+    lat, gu, wu = [], [], []
+    for b in range(first, first + batches):
+        batch = W.generate_batch_of_edges(5000, n, b, False, False, device=dev)
+        for ins in ((True, False) if mixed else (True,)):
+            t1 = time.perf_counter()
+            (g.insert_edges_batch if ins else g.delete_edges_batch)(batch, remove_dups=True, out=out)
+            lat.append((time.perf_counter() - t1) * 1e3)
+            st = g.stats()
+            gu.append(st["last_graph_update_ms"])
+            wu.append(st["last_walk_update_ms"])
+    return {"batch_median_ms": round(float(np.median(lat)), 3), "graph_update_median_ms": round(float(np.median(gu)), 3),
+            "walk_update_median_ms": round(float(np.median(wu)), 3)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -611,28 +855,12 @@ def main():
     bytes_per_step = BYTES_PER_STEP_DEEPWALK if args.model == "deepwalk" or args.det else BYTES_PER_STEP_NODE2VEC
     tag = f"gen_{args.model}_{'det' if args.det else 'mh'}_s{args.scale}"
 
-    # corpus reassembly for the downstream consumer: full-mesh all-gatherv over RCCL (not timed in `value`)
+    # corpus reassembly for the downstream consumer: bounded full-mesh all-gatherv over RCCL (not timed in `value`)
     corpus = None
     if dist:
-        from dynamicgraphrepresentationlearning_amd.distributed import allgatherv_corpus
-        loc = torch.empty((g.number_of_walks, args.length), dtype=torch.int32, device=f"cuda:{dev}")
-        g.export_walks_device(loc.data_ptr(), layout="walk")
-        # the whole corpus on every rank (received in place: the output is the
-        # only buffer), or its first rounds when it would not fit in the free
-        # HBM (gloo rehearsal: <= 16 GiB of host memory); local rows are round-major
-        round_bytes = max(n * args.length * 4, 1)
-        room = (16 << 30) if comm_dev == "cpu" else torch.cuda.mem_get_info(dev)[0] - (8 << 30)
-        rounds = max(1, min(wpv, room // round_bytes))
-        loc = loc[: (hi - lo) * rounds].to(comm_dev)
-        barrier()
-        t1 = time.perf_counter()
-        full = allgatherv_corpus(loc, shards, n, rounds)
-        barrier()
-        gms = (time.perf_counter() - t1) * 1e3
-        recv = full.numel() * 4 - loc.numel() * 4
-        corpus = {"ms": round(gms, 3), "rounds": rounds, "of_rounds": wpv, "bytes_received_per_rank": int(recv),
-                  "GBps_per_rank": round(recv / gms / 1e6, 1), "pattern": "batch_isend_irecv full mesh"}
-        del full, loc
+        free = torch.cuda.mem_get_info(dev)[0] if comm_dev != "cpu" else (8 << 30)
+        corpus = corpus_gather_record(args, torch, dist, g, shards, n, wpv, args.length, dev, comm_dev, world, rank,
+                                      barrier, max(64 << 20, min(args.gather_chunk_bytes, free // 4)))
     g.destroy()
 
     # strong scaling beside the weak line: configs[1] exactly (10 walks per vertex) split N ways
@@ -669,6 +897,15 @@ def main():
     if world == 1 and args.per_gpu_of_8 and args.model == "deepwalk" and not args.det:
         torch.cuda.empty_cache()
         per8 = per_gpu_of_8(args, W, torch, dev, barrier)
+
+    # BASELINE's two 8-GPU jobs on the ranks of this run (configs[3] strong, configs[4] g-of-8 weak)
+    jobs = None
+    if world > 1 and args.jobs and args.model == "deepwalk" and not args.det:
+        jobs = {}
+        for name in [j for j in args.jobs.split(",") if j]:
+            torch.cuda.empty_cache()
+            jobs[name] = multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrier)
+            log(f"[rank {rank}] job {name}: {json.dumps(jobs[name])}")
 
     if rank == 0:
         if rewalk and live_ceiling and bytes_per_step == BYTES_PER_STEP_DEEPWALK:
@@ -708,6 +945,7 @@ def main():
                          "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3), live_ceiling)
                          if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None},
             "per_gpu_of_8": per8,
+            "jobs_8gpu": jobs,
             "mh_accept_rate": round(st["accepts"] / st["steps"], 5) if st["steps"] else None,
             "strong_scaling": strong,
             "mh_node2vec": n2v,

@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # WHARF_LIB_PATH: an alternative build of the same library (A/B experiments in tools/)
 LIB_PATH = os.environ.get("WHARF_LIB_PATH") or os.path.join(_HERE, "libwharf_gpu.so")
 
-ABI_VERSION = 4   # WHARF_ABI_VERSION of include/wharf_gpu.h
+ABI_VERSION = 5   # WHARF_ABI_VERSION of include/wharf_gpu.h
 WHARF_OK = 0
 WHARF_DEEPWALK, WHARF_NODE2VEC = 0, 1
 WHARF_INIT_RANDOM, WHARF_INIT_BURNIN, WHARF_INIT_WEIGHT = 0, 1, 2
@@ -103,6 +103,8 @@ SIGNATURES = {
     "wharf_vertex_at_walk": (_I, [_P, _U64, _U32, _P]),
     "wharf_export_walks": (_I, [_P, _P, _I]),
     "wharf_export_walks_device": (_I, [_P, _P, _I]),
+    "wharf_export_walk_rows": (_I, [_P, _U64, _U64, _P]),
+    "wharf_export_walk_rows_device": (_I, [_P, _U64, _U64, _P]),
     "wharf_walk_ids": (_I, [_P, _P]),
     "wharf_index_size": (_I, [_P, _P]),
     "wharf_export_index": (_I, [_P, _P, _P, _P]),

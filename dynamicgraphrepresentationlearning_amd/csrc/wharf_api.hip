@@ -11,6 +11,7 @@
 #include <rocprim/iterator/counting_iterator.hpp>
 
 #include <charconv>
+#include <unistd.h>
 #include <chrono>
 #include <stdexcept>
 #include <string>
@@ -118,50 +119,90 @@ struct wharf_handle {
     // reference's corpus export calls walk(i) once per walk
     // (vertex-classification.cpp:145-148), which at one kernel + D2H + sync per
     // call is ~10^4 round trips per 10^4 walks.  Chunks of kSnapWalks walks are
-    // gathered walk-major on the device and copied to pinned host memory on
-    // first use; every change to the walks (walks_version) invalidates them.
+    // gathered walk-major on the device and copied to pinned host memory once
+    // kSnapFillAfter different walks of the chunk were read since the last
+    // change; sparser reads (the affected walks of a small batch,
+    // vertex-classification.cpp:171-176) read their own row from the device
+    // instead of pulling a whole chunk.  Every change to the walks
+    // (walks_version) invalidates both, and releases all but kSnapKeep chunks.
     static constexpr uint64_t kSnapWalks = 1ull << 16;
-    static constexpr size_t kSnapMaxChunks = 256;   // <= 16 GiB of pinned memory at L = 255
+    static constexpr uint32_t kSnapFillAfter = 32;   // distinct walks of a chunk read before the chunk is taken
+    static constexpr size_t kSnapKeep = 4;           // pinned chunks kept across a change of the walks
     struct Snap {
         uint64_t chunk = ~0ull;
         uint32_t* host = nullptr;
     };
     uint64_t walks_version = 0, snap_version = ~0ull;
     std::vector<Snap> snaps;
-    std::vector<int64_t> snap_of;   // chunk -> slot in snaps, or -1
-    size_t snap_next = 0;
+    std::vector<int64_t> snap_of;     // chunk -> slot in snaps, or -1
+    std::vector<uint32_t> snap_reads; // chunk -> walks read from it one by one since the last change
+    size_t snap_next = 0, snap_cap = 0;
+    std::vector<uint32_t> one_row;    // the last walk read on its own (vertex_at_walk(i, p) for p = 0, 1, ...)
+    uint64_t one_li = ~0ull, one_version = ~0ull;
 
     void walks_changed() { walks_version++; }
 
-    // walk-major row (L entries) of owned walk li, from the snapshot
+    // pinned chunks at most: 1/8 of the host's available memory, 4..256 chunks
+    // (20 MB each at L = 80; 8 ranks on one node each take their own)
+    size_t snap_max_chunks()
+    {
+        if (!snap_cap) {
+            const uint64_t bytes = kSnapWalks * L * 4;
+            const uint64_t avail = (uint64_t)sysconf(_SC_AVPHYS_PAGES) * (uint64_t)sysconf(_SC_PAGESIZE);
+            snap_cap = (size_t)std::min<uint64_t>(256, std::max<uint64_t>(4, avail / 8 / std::max<uint64_t>(bytes, 1)));
+        }
+        return snap_cap;
+    }
+
+    // walk-major row (L entries) of owned walk li: from the snapshot, or read on its own
     const uint32_t* snap_row(uint64_t li)
     {
         const uint64_t nchunks = (W + kSnapWalks - 1) / kSnapWalks, c = li / kSnapWalks;
         if (snap_version != walks_version || snap_of.size() != nchunks) {
+            // the snapshot is stale: drop it, and hand back all but a few pinned chunks
+            while (snaps.size() > kSnapKeep) {
+                if (snaps.back().host) (void)hipHostFree(snaps.back().host);
+                snaps.pop_back();
+            }
+            snap_next = 0;
             snap_of.assign(nchunks, -1);
+            snap_reads.assign(nchunks, 0);
             for (Snap& x : snaps) x.chunk = ~0ull;
             snap_version = walks_version;
         }
-        if (snap_of[c] < 0) {
-            size_t slot;
-            if (snaps.size() < kSnapMaxChunks) {
-                snaps.emplace_back();
-                slot = snaps.size() - 1;
-                HIPCHK(hipHostMalloc((void**)&snaps[slot].host, kSnapWalks * L * 4, hipHostMallocDefault));
-            } else {
-                slot = snap_next;
-                snap_next = (snap_next + 1) % kSnapMaxChunks;
-                if (snaps[slot].chunk != ~0ull) snap_of[snaps[slot].chunk] = -1;
-            }
-            const uint64_t base = c * kSnapWalks, cnt = std::min(kSnapWalks, W - base);
-            sel.ensure(kSnapWalks * L * 4);
-            launch_gather_rows(walks.as<uint32_t>(), W, L, nullptr, base, cnt, sel.as<uint32_t>(), s);
-            HIPCHK(hipMemcpyAsync(snaps[slot].host, sel.p, cnt * L * 4, hipMemcpyDeviceToHost, s));
+        if (snap_of[c] >= 0) return snaps[snap_of[c]].host + (li - c * kSnapWalks) * L;
+        if (one_version == walks_version && one_li == li) return one_row.data();
+        if (snap_reads[c] < kSnapFillAfter) {   // sparse so far: this row alone
+            snap_reads[c]++;
+            one_row.resize(L);
+            sel.ensure(L * 4);
+            launch_gather_rows(walks.as<uint32_t>(), W, L, nullptr, li, 1, sel.as<uint32_t>(), s);
+            HIPCHK(hipMemcpyAsync(one_row.data(), sel.p, L * 4, hipMemcpyDeviceToHost, s));
             sync();
-            snaps[slot].chunk = c;
-            snap_of[c] = (int64_t)slot;
+            one_li = li;
+            one_version = walks_version;
+            return one_row.data();
         }
-        return snaps[snap_of[c]].host + (li - c * kSnapWalks) * L;
+        size_t slot;
+        if (snaps.size() < snap_max_chunks()) {
+            uint32_t* p = nullptr;
+            HIPCHK(hipHostMalloc((void**)&p, kSnapWalks * L * 4, hipHostMallocDefault));
+            snaps.push_back(Snap{~0ull, p});   // only once the allocation succeeded
+            slot = snaps.size() - 1;
+        } else {
+            slot = snap_next;
+            snap_next = (snap_next + 1) % snaps.size();
+            if (snaps[slot].chunk != ~0ull) snap_of[snaps[slot].chunk] = -1;
+            snaps[slot].chunk = ~0ull;
+        }
+        const uint64_t base = c * kSnapWalks, cnt = std::min(kSnapWalks, W - base);
+        sel.ensure(kSnapWalks * L * 4);
+        launch_gather_rows(walks.as<uint32_t>(), W, L, nullptr, base, cnt, sel.as<uint32_t>(), s);
+        HIPCHK(hipMemcpyAsync(snaps[slot].host, sel.p, cnt * L * 4, hipMemcpyDeviceToHost, s));
+        sync();
+        snaps[slot].chunk = c;
+        snap_of[c] = (int64_t)slot;
+        return snaps[slot].host + (li - base) * L;
     }
     void free_snaps()
     {
@@ -169,7 +210,9 @@ struct wharf_handle {
             if (x.host) (void)hipHostFree(x.host);
         snaps.clear();
         snap_of.clear();
+        snap_reads.clear();
         snap_next = 0;
+        one_li = ~0ull;
     }
 
     void sync() { HIPCHK(hipStreamSynchronize(s)); }
@@ -281,8 +324,16 @@ struct wharf_handle {
     {
         const uint64_t pc = pool_capacity(pool_used, extra);
         const uint64_t need = pc * (4 + sizeof(ERec) * rec_stride()) + 3 * (n + 1) * 8 + (256ull << 20);
-        if (need <= free_bytes()) repack(extra);
-        else compact();
+        if (need <= free_bytes()) {
+            try {
+                repack(extra);
+                return;
+            } catch (const WharfError& e) {   // the second pool did not fit after all (fragmentation, a short
+                if (e.code != WHARF_E_NOMEM) throw;   // estimate): repack() left the handle as it was
+                (void)hipGetLastError();
+            }
+        }
+        compact();
     }
 
     // Fresh slack for every row, in a new pool with room for `extra` more slots
@@ -1439,6 +1490,42 @@ int wharf_export_walks_device(wharf_handle* h, uint32_t* dst, int layout)
     return guarded(h, [&] { export_walks_impl(h, dst, layout, hipMemcpyDeviceToDevice); });
 }
 
+// walk-major rows [first, first + count) of this handle's export order (the
+// rows wharf_export_walks(layout 0) writes there), without the whole corpus:
+// the bounded corpus gather (distributed.py) reads one chunk at a time
+static void export_rows_impl(wharf_handle* h, uint64_t first, uint64_t count, uint32_t* dst, bool device)
+{
+    REQUIRE(h, WHARF_E_INVALID, "null handle");
+    REQUIRE(first <= h->W && count <= h->W - first, WHARF_E_RANGE, "rows outside the handle's walks");
+    if (!count) return;
+    REQUIRE(dst, WHARF_E_INVALID, "null argument");
+    h->ensure_walks();
+    if (device) {
+        launch_gather_rows(h->walks.as<uint32_t>(), h->W, h->L, nullptr, first, count, dst, h->s);
+    } else {
+        const uint64_t chunk = 1ull << 20;   // staging bounded to 1 Mi rows
+        for (uint64_t c0 = 0; c0 < count; c0 += chunk) {
+            const uint64_t c = std::min(chunk, count - c0);
+            h->sel.ensure(c * h->L * 4);
+            launch_gather_rows(h->walks.as<uint32_t>(), h->W, h->L, nullptr, first + c0, c, h->sel.as<uint32_t>(), h->s);
+            HIPCHK(hipMemcpyAsync(dst + c0 * h->L, h->sel.p, c * h->L * 4, hipMemcpyDeviceToHost, h->s));
+            h->sync();
+        }
+    }
+    HIPCHK(hipGetLastError());
+    h->sync();
+}
+
+int wharf_export_walk_rows(wharf_handle* h, uint64_t first, uint64_t count, uint32_t* dst)
+{
+    return guarded(h, [&] { export_rows_impl(h, first, count, dst, false); });
+}
+
+int wharf_export_walk_rows_device(wharf_handle* h, uint64_t first, uint64_t count, uint32_t* dst_device)
+{
+    return guarded(h, [&] { export_rows_impl(h, first, count, dst_device, true); });
+}
+
 int wharf_write_corpus(wharf_handle* h, const char* path, const uint32_t* wids, uint64_t count, int append)
 {
     return guarded(h, [&] {
@@ -1658,11 +1745,12 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     r.records_bytes -= anchor_part;
     r.samplers_bytes = anchor_part + h->row_epoch.cap;
     r.edge_hash_bytes = h->ehash.cap + h->fdir.cap + h->fpool.cap;
-    r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->erec2.cap + h->scratch.cap + h->rplan.cap + h->pscan.cap;
+    r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->erec2.cap + h->scratch.cap + h->rplan.cap + h->pscan.cap +
+                             h->sanc.cap;   // the anchor carry's saved entries (8 B per saved slot)
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
                       h->runs.cap + h->fplan.cap + h->memo.cap + h->srcidx.cap + h->count.cap + h->pairs.cap +
                       h->sel.cap + h->defer.cap + h->park.cap + h->parkc.cap + h->stab.cap + h->preoff.cap + h->rtab.cap + h->bitmap.cap + h->counters.cap +
-                      h->errflag.cap;
+                      h->errflag.cap + h->bdesc.cap;
     r.total_bytes = r.csr_bytes + r.records_bytes + r.walks_bytes + r.samplers_bytes + r.edge_hash_bytes +
                     r.update_buffers_bytes + r.scratch_bytes;
     *out = r;

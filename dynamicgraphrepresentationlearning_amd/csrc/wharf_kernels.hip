@@ -171,7 +171,13 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
 // which is reset only when cur is a batch source (wharfmh.h:504,539): the
 // anchor stays valid while cur's row is unchanged since the tag (checked here)
 // AND while prev's row is unchanged — the entry sits in prev's row, which a
-// batch rebuilds with empty entries (k_erec_rows).  That second
+// batch with prev as a source rebuilds.  On a directed graph (or with
+// WHARF_ANCHOR_CARRY=0) the rebuilt row's entries start empty (k_erec_rows);
+// on an undirected graph the anchor carry keeps them through the merge
+// (k_save_rows / k_merge_rows) and k_anchor_invalidate resets only the entries
+// (y, prev) with y in N(prev) and in a changed edge's other end's filter — the
+// only states whose re-initialisation could pick differently — so a kept entry
+// equals what re-initialising would compute.  That prev-row
 // reset is a deliberate divergence: the reference's surviving
 // sampler was initialised against prev's row as it was at the first visit, a
 // function of which walks visited the state when, which differs per GPU shard;

@@ -13,6 +13,19 @@ vertex-classification.cpp:142-158): a full-mesh exchange of batched
 point-to-point sends/receives (torch.distributed.batch_isend_irecv, RCCL over
 xGMI with backend "nccl", gloo on CPU) — every peer pair uses its own link at
 once instead of a ring, and shards of different sizes need no padding.
+
+Two forms:
+  * allgatherv_corpus: the whole [n*wpv, L] corpus on every rank (fits while
+    the corpus is small next to the graph: configs[1]-[3]);
+  * gather_corpus_chunked: bounded memory, for corpora larger than a device
+    (configs[4]: 656 M walks x 80 x 4 B = 210 GB against 288 GB of HBM, 253 GB
+    of which the rank's graph and shard already hold).  Chunk c is local rows
+    [c*K, (c+1)*K) of EVERY rank, so each chunk is a full-mesh exchange; the
+    chunk lands in one buffer of K * world rows (or K rows on a rank that only
+    sends, gatherv to a root), is handed to a sink with the global walk ids of
+    its row runs, and the buffer is reused.  Local rows come from a callback
+    (WharfMH.export_walk_rows: one device gather per chunk), so neither the
+    corpus nor the rank's own walk-major copy is ever whole in memory.
 """
 from __future__ import annotations
 
@@ -79,3 +92,124 @@ def allgatherv_corpus(local_walks, shards, n: int, wpv: int, group=None):
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
     return out
+
+
+def local_rows_to_global(lo: int, hi: int, n: int, first: int, count: int):
+    """Global walk-id runs of local rows [first, first + count) of shard [lo, hi)
+    (local row i = round i // (hi-lo), vertex lo + i % (hi-lo)):
+    [(local_first, count, global_first)], each run inside one round."""
+    own = hi - lo
+    runs, i, end = [], first, first + count
+    while i < end:
+        r, j = divmod(i, own)
+        c = min(end - i, own - j)
+        runs.append((i, c, r * n + lo + j))
+        i += c
+    return runs
+
+
+def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per_rank: int, sink=None,
+                          root: int | None = None, group=None, device="cpu", dtype=None):
+    """Bounded-memory corpus gather: all-gatherv (root None) or gatherv to `root`.
+
+    read_local(first, count, out): writes this rank's walk-major local rows
+        [first, first + count) into the contiguous 2-D tensor `out` ([count, L]);
+    sink(chunk, segments): called on every receiving rank once per chunk, with
+        chunk = [R, L] tensor (valid until sink returns) and segments =
+        [(chunk_row, count, global_walk_id_first)] covering its R rows.
+    At most rows_per_rank * world rows (rows_per_rank on a sending-only rank)
+    are resident.  Returns {"chunks", "bytes_received", "bytes_sent"} of this rank.
+    """
+    import torch
+    import torch.distributed as dist
+
+    dtype = dtype or torch.int32
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    owns = [(hi - lo) * wpv for lo, hi in shards]
+    if len(owns) != world:
+        raise ValueError(f"{len(owns)} shards for a world of {world}")
+    K = max(1, int(rows_per_rank))
+    nchunks = -(-max(owns) // K) if max(owns) else 0
+    receives = root is None or rank == root
+    buf = torch.empty((K * (world if receives else 1), L), dtype=dtype, device=device)
+    cuda = buf.is_cuda
+    stats = {"chunks": nchunks, "bytes_received": 0, "bytes_sent": 0}
+    for c in range(nchunks):
+        parts = [(min(c * K, own), min((c + 1) * K, own)) for own in owns]
+        cnt = [b - a for a, b in parts]
+        base, acc = [], 0
+        for g in range(world):
+            base.append(acc if receives else 0)
+            if receives:
+                acc += cnt[g]
+        my0 = base[rank] if receives else 0
+        mine = buf[my0:my0 + cnt[rank]]
+        if cnt[rank]:
+            read_local(parts[rank][0], cnt[rank], mine)
+        ops = []
+        for peer in range(world):
+            if peer == rank:
+                continue
+            peer_receives = root is None or peer == root
+            if cnt[rank] and peer_receives:
+                ops.append(dist.P2POp(dist.isend, mine, peer, group))
+                stats["bytes_sent"] += mine.numel() * mine.element_size()
+            if receives and cnt[peer]:
+                dst = buf[base[peer]:base[peer] + cnt[peer]]
+                ops.append(dist.P2POp(dist.irecv, dst, peer, group))
+                stats["bytes_received"] += dst.numel() * dst.element_size()
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        if cuda:   # the library's export of the next chunk runs on its own stream: the buffer must be free
+            torch.cuda.current_stream(buf.device).synchronize()
+        if receives and sink is not None:
+            segs = []
+            for g, (lo, hi) in enumerate(shards):
+                if cnt[g]:
+                    for lf, k, gf in local_rows_to_global(lo, hi, n, parts[g][0], cnt[g]):
+                        segs.append((base[g] + lf - parts[g][0], k, gf))
+            sink(buf[:sum(cnt)], segs)
+            if cuda:
+                torch.cuda.current_stream(buf.device).synchronize()
+    return stats
+
+
+_K1 = 0x9E3779B97F4A7C15 - (1 << 64)   # as signed int64 (torch has no uint64 arithmetic)
+_K2 = 0xBF58476D1CE4E5B9 - (1 << 64)
+
+
+def corpus_checksum(rows, global_first: int, L: int, block_rows: int = 1 << 16):
+    """Order-independent checksum of walk-major rows whose first row is walk id
+    `global_first` (consecutive ids): sum over entries of (value + 1) * mix(id*L + pos),
+    int64 wrapping (mod 2^64).  The checksum of a whole corpus is the sum of its
+    pieces', so the sum of every rank's local checksum must equal the checksum
+    of what a gather delivered (the full-size property of bench.py's gather)."""
+    import torch
+
+    total = torch.zeros((), dtype=torch.int64, device=rows.device)
+    pos = torch.arange(L, dtype=torch.int64, device=rows.device)
+    for r0 in range(0, rows.shape[0], block_rows):
+        blk = rows[r0:r0 + block_rows]
+        ids = torch.arange(global_first + r0, global_first + r0 + blk.shape[0], dtype=torch.int64, device=rows.device)
+        h = (ids[:, None] * L + pos[None, :]) * _K1
+        h = (h ^ (h >> 31)) * _K2
+        total += (((blk.to(torch.int64) & 0xFFFFFFFF) + 1) * h).sum()
+    return total
+
+
+def local_corpus_checksum(read_local, lo: int, hi: int, n: int, wpv: int, L: int, rows_per_call: int,
+                          device="cpu"):
+    """corpus_checksum of this rank's own walks, read chunk by chunk."""
+    import torch
+
+    own = (hi - lo) * wpv
+    buf = torch.empty((max(1, min(rows_per_call, own)), L), dtype=torch.int32, device=device)
+    total = torch.zeros((), dtype=torch.int64, device=device)
+    for f in range(0, own, buf.shape[0]):
+        k = min(buf.shape[0], own - f)
+        read_local(f, k, buf[:k])
+        for lf, c, gf in local_rows_to_global(lo, hi, n, f, k):
+            total += corpus_checksum(buf[lf - f:lf - f + c], gf, L)
+    return total

@@ -279,6 +279,25 @@ class WharfMH:
         L.check(L.lib.wharf_export_walks_device(self._h, C.c_void_p(device_ptr), 0 if layout == "walk" else 1),
                 self._h, "export_walks_device")
 
+    def export_walk_rows(self, first: int, count: int, out=None) -> np.ndarray:
+        """Walk-major rows [first, first + count) of walks() (the handle's owned
+        walks in ascending id), one bounded chunk of the corpus.  `out`: a host
+        uint32 array of >= count * L entries, or a contiguous 32-bit torch tensor
+        on this handle's GPU (the rows stay in HBM: the chunked corpus gather)."""
+        Lw = self.config.walk_length
+        if out is not None and getattr(out, "is_cuda", False):
+            import torch
+            if out.dtype not in (torch.int32, torch.uint32) or out.numel() < count * Lw or not out.is_contiguous():
+                raise ValueError("device out must be a contiguous 32-bit tensor with >= count * walk_length entries")
+            L.check(L.lib.wharf_export_walk_rows_device(self._h, first, count, C.c_void_p(out.data_ptr())), self._h,
+                    "export_walk_rows_device")
+            return out
+        buf = out if out is not None else np.empty((count, Lw), dtype=np.uint32)
+        if buf.dtype != np.uint32 or buf.size < count * Lw or not buf.flags.c_contiguous:
+            raise ValueError("out must be a contiguous uint32 array with >= count * walk_length entries")
+        L.check(L.lib.wharf_export_walk_rows(self._h, first, count, _ptr(buf)), self._h, "export_walk_rows")
+        return buf
+
     def write_corpus(self, path: str, walk_ids=None, append: bool = False) -> None:
         """Text corpus for yskip (vertex-classification.cpp:142-150): one
         WharfMH::walk line per walk; all owned walks, or `walk_ids` in order."""

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define WHARF_ABI_VERSION 4
+#define WHARF_ABI_VERSION 5
 
 enum {
     WHARF_OK = 0,
@@ -177,6 +177,12 @@ int wharf_vertex_at_walk(wharf_handle* h, uint64_t wid, uint32_t position, uint3
  * a device pointer on the handle's device (used for the RCCL corpus gather). */
 int wharf_export_walks(wharf_handle* h, uint32_t* dst, int layout);
 int wharf_export_walks_device(wharf_handle* h, uint32_t* dst_device, int layout);
+/* Walk-major rows [first, first + count) of the layout-0 export (row i = the
+ * handle's i-th owned walk in ascending walk id), so a corpus can leave the
+ * device one bounded chunk at a time (the chunked corpus gather of
+ * distributed.py; vertex-classification.cpp:142-158 consumes the corpus). */
+int wharf_export_walk_rows(wharf_handle* h, uint64_t first, uint64_t count, uint32_t* dst);
+int wharf_export_walk_rows_device(wharf_handle* h, uint64_t first, uint64_t count, uint32_t* dst_device);
 /* global walk id of each owned walk, in export row order (walks entries). */
 int wharf_walk_ids(wharf_handle* h, uint32_t* ids_out);
 

@@ -26,7 +26,8 @@ import torch  # noqa: E402  (before the library: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
 import dynamicgraphrepresentationlearning_amd as W  # noqa: E402
-from dynamicgraphrepresentationlearning_amd.distributed import allgatherv_corpus, balanced_shards  # noqa: E402
+from dynamicgraphrepresentationlearning_amd.distributed import allgatherv_corpus, balanced_shards, \
+    corpus_checksum, gather_corpus_chunked, local_corpus_checksum  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 
@@ -75,6 +76,31 @@ def main():
         g.export_walks_device(loc.data_ptr(), layout="walk")
         torch.cuda.synchronize(dev)
         full = allgatherv_corpus(loc.cpu(), shards, n, wpv).numpy().view(np.uint32)
+        # the bounded form bench.py uses at configs[4]: chunks of local rows read from the
+        # handle one at a time (device rows staged to the host for gloo), checksum of checksums
+        dloc = torch.empty((1000, L), dtype=torch.int32, device=f"cuda:{dev}")
+
+        def read_local(first, count, out):
+            d = dloc[:count]
+            g.export_walk_rows(first, count, d)
+            out.copy_(d.cpu())
+            # the host form of the same rows
+            assert np.array_equal(g.export_walk_rows(first, count), out.numpy().view(np.uint32))
+
+        got = np.zeros_like(full)
+        acc = [torch.zeros((), dtype=torch.int64)]
+
+        def sink(chunk, segs):
+            for r0, c, g0 in segs:
+                got[g0:g0 + c] = chunk[r0:r0 + c].numpy().view(np.uint32)
+                acc[0] += corpus_checksum(chunk[r0:r0 + c], g0, L)
+
+        gather_corpus_chunked(read_local, shards, n, wpv, L, 1000, sink)
+        mine = local_corpus_checksum(read_local, lo, hi, n, wpv, L, 1000)
+        dist.all_reduce(mine)
+        chunked_ok = bool(np.array_equal(got, full)) and int(acc[0]) == int(mine)
+        ok_all = torch.tensor([int(chunked_ok)], dtype=torch.int64)
+        dist.all_reduce(ok_all, op=dist.ReduceOp.MIN)
         # the affected ids of all ranks (gathered through the same collective as counts)
         aff_all = None
         if local_aff is not None:
@@ -87,7 +113,8 @@ def main():
             rec = {"tag": tag,
                    "corpus_eq_single": bool(np.array_equal(full, single.walks())),
                    "corpus_eq_oracle": bool(np.array_equal(full, ref.walks())),
-                   "steps_eq": int(steps.item()) == int(ref.steps)}
+                   "steps_eq": int(steps.item()) == int(ref.steps),
+                   "chunked_eq": bool(ok_all.item())}
             if aff_all is not None:
                 rec["affected_eq"] = bool(np.array_equal(aff_all, report["_ref_aff"]))
             report["steps"].append(rec)

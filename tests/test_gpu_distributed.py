@@ -1,6 +1,7 @@
 """Multi-process HIP path on the GPU box: N ranks (gloo, one process each), every
 rank with its own libwharf_gpu.so handle over its start-vertex shard, corpus
-reassembled by distributed.allgatherv_corpus from device exports — bit-exact
+reassembled by distributed.allgatherv_corpus from device exports and by the
+bounded distributed.gather_corpus_chunked from per-chunk device row exports — bit-exact
 against one unsharded handle and the CPU oracle after generation and after
 every batch of a configs[4]-shaped node2vec MH stream (mixed insert/delete) and
 a configs[3]-shaped deterministic DeepWalk stream.  (The RCCL backend runs the
@@ -38,5 +39,5 @@ def test_sharded_handles_reproduce_the_single_corpus(tmp_path, mode, world):
     rep = json.load(open(out))
     assert rep["world"] == world and len(rep["steps"]) >= 5
     for st in rep["steps"]:
-        assert st["corpus_eq_single"] and st["corpus_eq_oracle"] and st["steps_eq"], st
+        assert st["corpus_eq_single"] and st["corpus_eq_oracle"] and st["steps_eq"] and st["chunked_eq"], st
         assert st.get("affected_eq", True), st

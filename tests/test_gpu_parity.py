@@ -588,6 +588,42 @@ def test_walk_readout_snapshot_follows_every_change(W, monkeypatch):
     g.destroy()
 
 
+def test_walk_rows_export_and_sparse_readout(W):
+    """wharf_export_walk_rows[_device] (one bounded chunk of the corpus, the
+    chunked corpus gather's source) equals the whole export on any row range;
+    walk() of a few walks per 64 Ki-walk chunk reads them one by one (ADVICE r3:
+    no chunk pulled for a sparse affected-walk readout), a dense readout takes the
+    chunk, and both agree with the export after every change."""
+    import torch
+    base = O.generate_batch_of_edges(60000, 1 << 18, 4, False, False)
+    off, adj = O.csr_from_edges(1 << 17, base)
+    cfg = W.WharfConfig(walks_per_vertex=2, walk_length=10, deterministic=True)
+    g = W.WharfMH.from_csr(off, adj, config=cfg)
+    g.generate_initial_random_walks()
+    full = g.walks()
+    Wn = g.number_of_walks
+    for first, count in ((0, 1), (0, Wn), (65535, 2), (100_000, 61_000), (Wn - 3, 3), (Wn, 0)):
+        assert np.array_equal(g.export_walk_rows(first, count), full[first:first + count])
+        d = torch.empty((max(count, 1), 10), dtype=torch.int32, device="cuda:0")
+        g.export_walk_rows(first, count, d)
+        assert np.array_equal(d[:count].cpu().numpy().view(np.uint32), full[first:first + count])
+    with pytest.raises(RuntimeError):
+        g.export_walk_rows(Wn - 1, 2)
+    for rnd in range(2):
+        # sparse: a few walks of each chunk, and every position of one walk
+        for c in range(0, Wn, 1 << 16):
+            for i in (c, c + 7, min(c + 40_000, Wn - 1)):
+                assert g.walk(i) == O.walk_string(full[i])
+        assert [g.vertex_at_walk(70_001, p) for p in range(10)] == [int(x) for x in full[70_001]]
+        # dense: one whole chunk walk by walk (the chunk is taken after 32 single reads)
+        for i in range(1 << 16, 1 << 17):
+            assert g.walk_vertices(i).tolist() == full[i][full[i] != W.SENTINEL].tolist()
+        b = O.generate_batch_of_edges(2000, 1 << 17, 20 + rnd, False, False)
+        g.insert_edges_batch(b, remove_dups=True)
+        full = g.walks()
+    g.destroy()
+
+
 # ---------------------------------------------------------------------------
 # MH mode
 # ---------------------------------------------------------------------------
