@@ -9,7 +9,8 @@ outputs for them.
 
     python tests/golden/make_golden.py            # writes tests/golden/*
     python tests/golden/make_golden.py mh-matrix  # only the MH statistics matrices (merged into golden.json)
-    python tests/golden/make_golden.py mh-stream  # only the MH stream cells
+    python tests/golden/make_golden.py mh-stream  # only the MH stream cells (wiki)
+    python tests/golden/make_golden.py mh-stream-rmat  # only the MH stream cells on the RMAT hub graph
 """
 from __future__ import annotations
 
@@ -246,6 +247,99 @@ def mh_stream_matrix(tmp, woff, wadj):
                          "<ins|del> <edges> <batch seed> <directed> x2 dump-graph, NUM_THREADS=1 (remove_dups=true)"}
 
 
+# RMAT stream cells (the prev-row reset and the anchor carry act per hub row, and
+# wiki has no hubs): an RMAT scale-12 graph (generate_batch_of_edges(40000, 8192, 5, false,
+# undirected) on n = 4096: max degree 421 against a mean of 18), without its isolated vertices
+# (a directed edge into one makes a sink, see wiki_compact), saved as rmat12c_csr.npz.
+#   undirected pairs: insert batch b, delete batch b, insert b + 50, delete b + 50
+#     (generate_batch_of_edges(600, n, ., false, undirected), throughput-latency.cpp:126,135), at
+#     (p, q) = (0.5, 2) with WEIGHT and with RANDOM inits;
+#   directed pair: insert a directed batch, delete it (throughput-latency.cpp:121,126,135), WEIGHT.
+RMAT_CELL_GRAPH = ("rmat12c", 40000, 8192, 5, 4096)   # name, samples, vertices_number, seed, n
+RMAT_PAIR_EDGES = 600
+RMAT_DIRECTED_EDGES = 1000
+
+
+def rmat_stream_cell_specs():
+    return [("rmat_undirected_p0.5_q2.0_weight", False, 0.5, 2.0, "weight"),
+            ("rmat_undirected_p0.5_q2.0_random", False, 0.5, 2.0, "random"),
+            ("rmat_directed_p0.5_q2.0_weight", True, 0.5, 2.0, "weight")]
+
+
+def rmat_cell_graph(tmp):
+    """The reference's own RMAT base graph (ref_harness graph-rmat + dump-graph),
+    isolated vertices removed."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import mh_stats
+    name, samples, vn, seed, n = RMAT_CELL_GRAPH
+    d = os.path.join(tmp, "rmatcell")
+    os.makedirs(d, exist_ok=True)
+    run(["out", d, "cfg", 1, 2, "deepwalk", 1, 1, "weight", 1, 1, "graph-rmat", samples, vn, seed, n, "gen", "dump-graph"])
+    off, adj = read_graph(d, "0")
+    return mh_stats.compact_graph(off, adj)
+
+
+def mh_stream_rmat_cells(tmp):
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, REPO)
+    import mh_stats
+    off, adj = rmat_cell_graph(tmp)
+    np.savez_compressed(os.path.join(HERE, f"{RMAT_CELL_GRAPH[0]}_csr.npz"), off=off, adj=adj)
+    csr = os.path.join(tmp, "rmat12c.csr")
+    write_csr(csr, off, adj)
+    dseeds = mh_stats.stream_batch_seeds(off, adj, len(MH_SEEDS), RMAT_DIRECTED_EDGES)
+    jobs, cells = [], {}
+    for key, directed, p, q, init in rmat_stream_cell_specs():
+        per_seed = []
+        for i, s in enumerate(MH_SEEDS):
+            if directed:
+                b = dseeds[i]
+                batches = [{"insert": True, "edges": RMAT_DIRECTED_EDGES, "seed": b, "directed": True},
+                           {"insert": False, "edges": RMAT_DIRECTED_EDGES, "seed": b, "directed": True}]
+            else:
+                batches = [{"insert": ins, "edges": RMAT_PAIR_EDGES, "seed": s + o, "directed": False}
+                           for o in (0, 50) for ins in (True, False)]
+            per_seed.append(batches)
+            jobs.append((tmp, csr, key, batches, p, q, init, s))
+        cells[key] = {"graph": RMAT_CELL_GRAPH[0], "directed": directed, "p": p, "q": q, "init": init,
+                      "batches": per_seed}
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        res = list(ex.map(_mh_stream_cell, jobs))
+    fr_by = {}
+    for j, fr in zip(jobs, res):
+        fr_by.setdefault(j[2], []).append(fr)
+    for key, fr in fr_by.items():
+        c = cells[key]
+        c["transitions"] = [f["transitions"] for f in fr]
+        for k in ("return", "triangle", "outward"):
+            v = np.array([f[k] for f in fr])
+            c[k] = {"mean": float(v.mean()), "sd": float(v.std(ddof=1)), "per_seed": [float(x) for x in v]}
+    return cells
+
+
+def main_mh_stream_rmat():
+    """Adds the RMAT stream cells to golden.json's mh_stream_matrix_reference."""
+    if not os.path.exists(HARNESS):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
+    tmp = tempfile.mkdtemp(prefix="golden_mhr_")
+    try:
+        cells = mh_stream_rmat_cells(tmp)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    path = os.path.join(HERE, "golden.json")
+    meta = json.load(open(path))
+    ms = meta["mh_stream_matrix_reference"]
+    ms["cells"].update(cells)
+    ms["graphs"][RMAT_CELL_GRAPH[0]] = (f"tests/golden/{RMAT_CELL_GRAPH[0]}_csr.npz: the reference's "
+                                        f"generate_batch_of_edges({RMAT_CELL_GRAPH[1]}, {RMAT_CELL_GRAPH[2]}, "
+                                        f"{RMAT_CELL_GRAPH[3]}, false, undirected) on n = {RMAT_CELL_GRAPH[4]} "
+                                        "(ref_harness graph-rmat), isolated vertices removed")
+    with open(path, "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("RMAT stream cells written to", path)
+
+
 def main_mh_matrix(stream_only=False):
     if not os.path.exists(HARNESS):
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
@@ -409,6 +503,7 @@ def main():
         meta["mh_stats_reference"] = mh
         meta["mh_matrix_reference"] = mh_matrix(tmp, woff, wadj)
         meta["mh_stream_matrix_reference"] = mh_stream_matrix(tmp, woff, wadj)
+        meta["mh_stream_matrix_reference"]["cells"].update(mh_stream_rmat_cells(tmp))
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     with open(os.path.join(HERE, "golden.json"), "w") as f:
@@ -421,4 +516,6 @@ if __name__ == "__main__":
         sys.exit(main_mh_matrix())
     if sys.argv[1:] == ["mh-stream"]:
         sys.exit(main_mh_matrix(stream_only=True))
+    if sys.argv[1:] == ["mh-stream-rmat"]:
+        sys.exit(main_mh_stream_rmat())
     sys.exit(main())

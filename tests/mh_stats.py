@@ -82,6 +82,11 @@ def wiki_compact(off: np.ndarray, adj: np.ndarray):
     graph of the directed stream cells.  A directed batch edge into an isolated
     vertex makes a sink, where the reference evaluates lrand() % 0
     (utility.h:220, via node2vec.h:97-105) and dies of SIGFPE."""
+    return compact_graph(off, adj)
+
+
+def compact_graph(off: np.ndarray, adj: np.ndarray):
+    """A CSR without its isolated vertices, ids renumbered in order."""
     off = off.astype(np.int64)
     deg = np.diff(off)
     keep = np.nonzero(deg > 0)[0]
@@ -125,8 +130,16 @@ def stream_batches(cell: dict, i: int, n: int, gen_batch):
 
 
 def stream_graph(cell: dict, off: np.ndarray, adj: np.ndarray):
-    """The cell's base graph from wiki's CSR."""
-    return wiki_compact(off, adj) if cell["graph"] == "wiki_compact" else (off, adj)
+    """The cell's base graph: wiki's CSR (off, adj), wiki without isolated
+    vertices, or a graph committed beside golden.json (tests/golden/<name>_csr.npz:
+    the RMAT hub graph of the rmat_* cells)."""
+    if cell["graph"] == "wiki_compact":
+        return wiki_compact(off, adj)
+    if cell["graph"] == "wiki":
+        return off, adj
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"{cell['graph']}_csr.npz"))
+    return z["off"], z["adj"]
 
 
 def stream_cells(matrix: dict):

@@ -17,7 +17,10 @@ bit for bit and the rest is checked structurally:
   of its round from its batch source on the new graph;
 
   configs[1] generation with node2vec MH (every anchor initialised, wave-
-  cooperatively): step count, transitions, a 4096-walk window vs the oracle.
+  cooperatively): step count, transitions, a 4096-walk window vs the oracle;
+
+  configs[3] / configs[4] per-GPU work of their 8-GPU runs (full graph, walk
+  shard 0 of 8): generation and update batches checked the same way.
 """
 import numpy as np
 import pytest
@@ -307,4 +310,106 @@ def test_configs3_full_size_shard_of_8(W, torch):
             walked += int(m.sum())
             assert _all_edges(torch, ekeys2, n, after[pos, m], after[pos + 1, m]), f"non-edge re-walk step at {pos}"
     assert walked == steps
+    g.destroy()
+
+
+def _csr_dev(torch, off, adj):
+    return torch.from_numpy(off.astype(np.int64)).cuda(), torch.from_numpy(adj.view(np.int32)).cuda()
+
+
+def _all_edges_csr(torch, doff, dadj, u, v):
+    """Every (u[i], v[i]) is an edge: a vectorised binary search of v in u's
+    (ascending) row of the device CSR — no per-edge key array (configs[4]'s
+    3.6 G edges as int64 keys would not fit beside the graph)."""
+    u, v = u.long(), v.long()
+    lo, end = doff[u], doff[u + 1]
+    hi = end.clone()
+    last = dadj.numel() - 1
+    while True:
+        act = lo < hi
+        if not bool(act.any()):
+            break
+        mid = (lo + hi) // 2
+        less = dadj[mid.clamp(max=last)].long() < v
+        lo = torch.where(act & less, mid + 1, lo)
+        hi = torch.where(act & ~less, mid, hi)
+    return bool(((lo < end) & (dadj[lo.clamp(max=last)].long() == v)).all())
+
+
+def test_configs4_full_size_shard_of_8(W, torch):
+    """configs[4]'s per-GPU work of its 8-GPU run at full graph size: the
+    friendster-sized RMAT graph (scale 26, 1.8 G undirected samples, ~3.6 G CSR
+    entries in a slot pool of ~4 G slots: 40-bit row offsets, 32-B node2vec
+    records with in-record anchors) with the walks of start-vertex shard 0 of 8,
+    node2vec p = .5 q = 2 MH with WEIGHT inits and the anchor carry on, one walk
+    per vertex (wpv 1 bounds the test's time; the bench runs wpv 10).
+    Generation: step count, starts, every sampled transition is an edge, a
+    4096-walk window equal to the oracle's.  Then one insert and one delete of
+    generate_batch_of_edges(5000, n, b, false, false) (throughput-latency.cpp:126,135):
+    affected ids are exactly the shard's walks holding a batch source, nothing
+    changes up to a walk's rewalk point, re-walked transitions are edges of the
+    new graph, the step counter matches."""
+    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards
+    n = 1 << 26
+    sent = int(np.uint32(W.SENTINEL).view(np.int32))
+    cfg = W.WharfConfig(walks_per_vertex=1, walk_length=L, model=W.NODE2VEC, paramP=0.5, paramQ=2.0,
+                        sampler_init=W.WEIGHT, deterministic=False, seed=0x5EED)
+    g = W.WharfMH.from_rmat(n, 1_800_000_000, 2 * n, seed=4, config=cfg)
+    st0 = g.stats()
+    assert st0["pool_capacity"] > (1 << 31) and g.number_of_edges() > 3_000_000_000
+    off, adj = g.flatten_graph()
+    deg_h = np.diff(off.astype(np.int64))
+    lo, hi = balanced_shards(deg_h, 8)[0]
+    g.set_shard(lo, hi)
+    nl = hi - lo
+    assert g.number_of_walks == nl
+    g.generate_initial_random_walks()
+    st = g.stats()
+    active = int((deg_h[lo:hi] > 0).sum())
+    assert st["steps"] == active * (L - 1) and 0 < st["accepts"] <= st["steps"] and st["last_anchor_inits"] > 0
+    before = _dev_walks(torch, g)
+    doff, dadj = _csr_dev(torch, off, adj)
+    start = lo + torch.arange(nl, device="cuda:0")
+    assert torch.equal(before[0].long(), start)
+    iso = torch.from_numpy(deg_h[lo:hi] == 0).cuda()
+    for p in (0, 1, 40, 78):
+        assert _all_edges_csr(torch, doff, dadj, before[p, ~iso], before[p + 1, ~iso]), f"non-edge transition at {p}"
+    # oracle window: the shard's first 4096 start vertices (= local columns 0..4095)
+    ref = O.Engine(off, adj, wpv=1, L=L, model=O.NODE2VEC, p=0.5, q=2.0, init=O.INIT_WEIGHT, deterministic=False,
+                   seed=0x5EED)
+    ref.time_generate_range(lo, lo + 4096)
+    mine = before[:, :4096].T.contiguous().cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(mine, ref.walks_range(lo, lo + 4096))
+    del ref, off, adj
+    ids = torch.empty(g.number_of_walks, dtype=torch.int32, device="cuda:0")
+    batch = W.generate_batch_of_edges(5000, n, 0, False, False)
+    for insert in (True, False):
+        aff = (g.insert_edges_batch if insert else g.delete_edges_batch)(batch, remove_dups=True, out=ids)
+        steps = g.stats()["steps"]
+        after = _dev_walks(torch, g)
+        is_src = torch.zeros(n, dtype=torch.bool, device="cuda:0")
+        is_src[torch.from_numpy(batch[:, 0].astype(np.int64)).cuda()] = True
+        p = torch.full((nl,), L, dtype=torch.int64, device="cuda:0")
+        for pos in range(L - 1, -1, -1):
+            row = before[pos]
+            hit = (row != sent) & is_src[row.clamp(min=0).long()]
+            p = torch.where(hit, torch.full_like(p, pos), p)
+        affected = p < L
+        assert torch.equal(aff.long(), start[affected])        # wpv 1: walk id = start vertex
+        del doff, dadj
+        torch.cuda.empty_cache()
+        o2, a2 = g.flatten_graph()
+        doff, dadj = _csr_dev(torch, o2, a2)
+        del o2, a2
+        walked = 0
+        for pos in range(L):
+            kept = pos <= p
+            assert torch.equal(after[pos][kept], before[pos][kept]), f"position {pos} changed before the rewalk point"
+            if pos + 1 < L:
+                m = affected & (pos >= p) & (after[pos + 1] != sent)
+                walked += int(m.sum())
+                assert _all_edges_csr(torch, doff, dadj, after[pos, m], after[pos + 1, m]), \
+                    f"non-edge re-walk step at {pos}"
+        assert walked == steps
+        before = after
     g.destroy()

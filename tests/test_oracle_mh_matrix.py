@@ -54,8 +54,11 @@ STREAM = json.load(open(os.path.join(G, "golden.json")))["mh_stream_matrix_refer
 
 def test_stream_matrix_covers_directed_and_undirected_cells():
     cells = STREAM["cells"]
-    assert len(cells) == 18                       # 3 (p, q) x 3 inits x {undirected, directed}
-    assert sum(c["directed"] for c in cells.values()) == 9
+    assert len(cells) == 21                       # wiki: 3 (p, q) x 3 inits x {undirected, directed}; RMAT: 3
+    assert sum(c["directed"] for c in cells.values()) == 10
+    rmat = [k for k, c in cells.items() if c["graph"] == "rmat12c"]
+    assert sorted(rmat) == ["rmat_directed_p0.5_q2.0_weight", "rmat_undirected_p0.5_q2.0_random",
+                            "rmat_undirected_p0.5_q2.0_weight"]
     for c in cells.values():
         assert len(c["return"]["per_seed"]) == len(STREAM["seeds"]) == len(c["batches"]) == 8
 
@@ -68,7 +71,8 @@ def test_oracle_mh_stream_vs_reference(wiki, cell):
     batches on wiki, and the reference driver's directed insert/delete pairs of
     one batch (throughput-latency.cpp:121,126,135) on wiki without isolated
     vertices — the batches where the prev-row anchor reset of DESIGN.md §4
-    departs from the reference's keep-first-anchor samplers."""
+    departs from the reference's keep-first-anchor samplers — and insert/delete
+    pairs (undirected: the anchor carry; directed) on an RMAT graph with hubs."""
     key, p, q, init = cell
     c = STREAM["cells"][key]
     off, adj = S.stream_graph(c, *wiki)
