@@ -595,6 +595,8 @@ struct wharf_handle {
         // 17.8-18.2 -> 17.1-17.3 ms at wpv 1 but 67-78 -> 73-82 ms at wpv 10, configs[2] +0.7 %,
         // profiles/r03/retfirst) need the return to be the one heaviest class (p < 1, p < q) and
         // proposals that need has_edge at all (q != 1)
+        a.err = errflag.as<unsigned long long>() + 5;   // re-walk list consumers (list_entry_ok)
+        a.stage = 0;
         const char* rf = getenv("WHARF_RET_FIRST");
         a.ret_first = cfg.model == WHARF_NODE2VEC && !cfg.deterministic && cfg.sampler_init == WHARF_INIT_WEIGHT &&
                       !a.no_sure && a.inv_q != 1.0f && a.inv_p > fmaxf(1.0f, a.inv_q) && rf && *rf && atoi(rf) != 0;
@@ -893,6 +895,39 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         const char* rw = getenv("WHARF_N2V_REWALK");
         a.park = a.model == kNode2Vec && !a.det && a.anchor && !a.scan_only && rw && std::string(rw) == "park";
         h->walks_changed();
+        HIPCHK(hipMemsetAsync(a.err, 0, 8, s));
+        // node2vec list order (tests): WHARF_N2V_LIST_ORDER=global sorts k_rewalk_plan's list by
+        // rewalk point over all blocks (round 3's global sort, rebuilt: the count masked out of the
+        // packed word, the sort's output apart from rocPRIM's temp storage) before the consumer;
+        // WHARF_TEST_CORRUPT_LIST=1 plants one out-of-range entry, which the consumer must report
+        // (WHARF_E_STATE) without touching memory through it
+        const char* lord = getenv("WHARF_N2V_LIST_ORDER");
+        const char* lbad = getenv("WHARF_TEST_CORRUPT_LIST");
+        const bool n2v_list = a.model == kNode2Vec && !a.det && !a.scan_only && !a.park && !a.bdesc;
+        const bool gsort = n2v_list && lord && std::string(lord) == "global";
+        const bool corrupt = n2v_list && lbad && atoi(lbad) != 0;
+        if (gsort || corrupt) {
+            a.stage = 1;
+            launch_walk(a, true, s);
+            uint64_t c2 = 0;
+            HIPCHK(hipMemcpyAsync(&c2, a.counters + 2, 8, hipMemcpyDeviceToHost, s));
+            h->sync();
+            const uint64_t cnt = c2 & kListMask;   // tickets << 40 | entries
+            REQUIRE(cnt <= h->W, WHARF_E_STATE, "re-walk list longer than the walks");
+            if (gsort && cnt > 1) {
+                h->park.ensure(cnt * 8);
+                uint64_t* in = h->defer.as<uint64_t>();
+                uint64_t* out = h->park.as<uint64_t>();
+                h->rp([&](void* t, size_t& b) { return rocprim::radix_sort_keys(t, b, in, out, (size_t)cnt, 56u, 64u, s); });
+                HIPCHK(hipMemcpyAsync(in, out, cnt * 8, hipMemcpyDeviceToDevice, s));
+            }
+            if (corrupt && cnt) {
+                const uint64_t bad = (h->W + 12345) | (1ull << 56);
+                HIPCHK(hipMemcpyAsync(h->defer.as<uint64_t>() + cnt / 2, &bad, 8, hipMemcpyHostToDevice, s));
+                h->sync();
+            }
+            a.stage = 2;
+        }
         launch_walk(a, true, s);
         HIPCHK(hipGetLastError());
         if (a.park) park_passes(h, a);
@@ -912,8 +947,13 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         launch_aff_write(h->aff.as<uint8_t>(), h->W, boff, h->n, h->n_loc, h->lo,
                          on_device ? affected_out : h->pairs.as<uint32_t>(), s);
         uint32_t naff32 = 0;
+        unsigned long long lerr = 0;
         HIPCHK(hipMemcpyAsync(&naff32, boff + nb, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&lerr, a.err, 8, hipMemcpyDeviceToHost, s));
         h->sync();
+        REQUIRE(lerr == 0, WHARF_E_STATE,
+                std::string("node2vec re-walk list: ") + ((lerr & 1) ? "an entry outside the walks" : "an entry outside its block") +
+                    " was skipped; the walks of this update are incomplete");
         const uint64_t naff = naff32;
         if (affected_out && !on_device && naff) {
             HIPCHK(hipMemcpyAsync(affected_out, h->pairs.p, naff * 4, hipMemcpyDeviceToHost, s));

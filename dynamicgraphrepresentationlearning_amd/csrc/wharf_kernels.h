@@ -60,6 +60,8 @@ struct WalkArgs {
     int lane_sort;               // node2vec sorted re-walk: a wave's 64 list entries in column order
     int src_exact;               // src_idx holds kNoSource for every non-source (the copy settles positives by it)
     int ret_first;               // node2vec MH, WEIGHT, 1/p the unique heaviest weight: return-first inits (walk_step)
+    unsigned long long* err;     // re-walk list consumers: bit 0 an entry out of range, bit 1 an entry outside its block
+    int stage;                   // node2vec re-walk launch: 0 plan + consumer, 1 plan only, 2 consumer only
 };
 
 constexpr uint64_t kListMask = (1ull << 40) - 1;   // counters[2]: tickets << 40 | re-walk list entries

@@ -1538,6 +1538,19 @@ __global__ __launch_bounds__(256) WHARF_SCAN_WAVES void k_rewalk_plan(WalkArgs a
     }
 }
 
+// An entry of the node2vec re-walk list names an owned walk (li < W) and a
+// rewalk point with a step after it (p + 1 < L), which k_rewalk_plan* always
+// write.  Anything else — a list that was corrupted or mis-sized between the
+// plan and its consumer (round 3: a global sort of the list faulted its first
+// GPU run) — is never dereferenced: the consumer skips it and
+// reports it through a.err, and the host fails the update with WHARF_E_STATE.
+__device__ __forceinline__ bool list_entry_ok(const WalkArgs& a, uint64_t li, uint32_t p)
+{
+    if (li < a.W && p + 1 < a.L) return true;
+    atomicOr(a.err, 1ull);
+    return false;
+}
+
 // Sort a wave's 64 re-walk list entries (walk | point << 56; ~0 = none) by walk
 // (column), ascending, so the nones end up last: bitonic over the lanes.
 __device__ __forceinline__ uint64_t wave_sort_entries(uint64_t ent)
@@ -1577,7 +1590,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
         // neighbouring lanes merge; a bitonic sort over the wave, 21 shuffle steps
         uint64_t ent = e < cnt ? a.defer[e] : ~0ull;
         if (a.lane_sort) ent = wave_sort_entries(ent);
-        const bool active = ent != ~0ull;
+        const bool active = ent != ~0ull && list_entry_ok(a, ent & ((1ull << 56) - 1), (uint32_t)(ent >> 56));
         uint64_t li = 0;
         uint32_t p = L, wlo = 0, whi = 0;
         const uint64_t* __restrict__ rt = nullptr;
@@ -1650,13 +1663,17 @@ __global__ __launch_bounds__(256) void k_rewalk_block(WalkArgs a)
         pcol[t] = kNoRewalk;
         if (t == 0) s_first = L;
         __syncthreads();
-        const bool active = t < cnt;
+        const uint64_t ent = t < cnt ? a.defer[(d & kListMask) + t] : 0ull;
+        // (also within this workgroup's 256-walk block: pcol is indexed by li - base)
+        const bool active = t < cnt && list_entry_ok(a, ent & ((1ull << 56) - 1), (uint32_t)(ent >> 56)) &&
+                            (ent & ((1ull << 56) - 1)) - base < 256;
         uint64_t li = 0;
         uint32_t p = L, wlo = 0, whi = 0;
         Walker w;
         w.rc.deg = 0;
+        if (t < cnt && !active && list_entry_ok(a, ent & ((1ull << 56) - 1), (uint32_t)(ent >> 56)))
+            atomicOr(a.err, 2ull);   // a valid walk outside the block: not this kernel's list
         if (active) {
-            const uint64_t ent = a.defer[(d & kListMask) + t];
             li = ent & ((1ull << 56) - 1);
             p = (uint32_t)(ent >> 56);
             const uint64_t r = li / a.n_loc;
@@ -1723,11 +1740,12 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
     Walker w;
     w.rc.deg = 0;
     for (;;) {
-        if (pos >= L && i < cnt) {   // next walk of this lane
+        while (pos >= L && i < cnt) {   // next walk of this lane (an entry out of range is skipped)
             const uint64_t e = a.defer[i];
             i += stride;
             li = e & ((1ull << 56) - 1);
             p = (uint32_t)(e >> 56);
+            if (!list_entry_ok(a, li, p)) continue;
             const uint64_t r = li / a.n_loc;
             const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
             wlo = (uint32_t)wid;
@@ -1797,11 +1815,15 @@ __global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* 
     w.rc.deg = 0;
     bool has = false;
     for (;;) {
-        if (!has && i < cnt) {   // this lane's next walker
+        while (!has && i < cnt) {   // this lane's next walker (a fresh entry out of range is skipped)
             if constexpr (FRESH) {
                 const uint64_t e = a.defer[i];
                 li = e & ((1ull << 56) - 1);
                 const uint32_t p = (uint32_t)(e >> 56);
+                if (!list_entry_ok(a, li, p)) {
+                    i += stride;
+                    continue;
+                }
                 pos = p + 1;
                 const uint64_t r = li / a.n_loc;
                 const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
@@ -1943,13 +1965,15 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
 #define WHARF_LAUNCH(M, D)                                                                   \
     do {                                                                                     \
         if (rewalk && M == kNode2Vec) {                                                      \
-            if (plan_lean) {                                                                 \
+            if (a.stage == 2) {                                                              \
+            } else if (plan_lean) {                                                          \
                 if (a.nt_rows) hipLaunchKernelGGL(k_rewalk_plan_lean<true>, pgrid, dim3(1024), 0, s, a); \
                 else hipLaunchKernelGGL(k_rewalk_plan_lean<false>, pgrid, dim3(1024), 0, s, a);  \
             } else {                                                                         \
                 hipLaunchKernelGGL(k_rewalk_plan, grid, block, 0, s, a);                     \
             }                                                                                \
-            if (!a.scan_only && !a.park) { /* park: the host runs the passes */              \
+            /* park: the host runs the passes; stage 1: the host reorders the list first */  \
+            if (!a.scan_only && !a.park && a.stage != 1) {                                   \
                 if (a.bdesc) hipLaunchKernelGGL((k_rewalk_block<M>), lgrid, block, 0, s, a);     \
                 else if (flat_list()) hipLaunchKernelGGL((k_rewalk_list<M, D>), lgrid, block, 0, s, a); \
                 else if (a.ret_first) hipLaunchKernelGGL((k_rewalk_sorted<M, D, M == kNode2Vec>), lgrid, block, 0, s, a); \

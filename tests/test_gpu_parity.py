@@ -363,6 +363,9 @@ def test_affected_ids_on_device_match_host_list(W):
 PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0", "on", "0", "1"),
          "park/slack": ("park", "0", "0", "on", "1", "0", "on", "1", "1"),
          "sorted/move-lazy": ("sorted", "1", "0", "on", "1", "0", "on", "1", "0"),
+         # round 3's faulted combination: move-lazy with the list sorted by rewalk point over all
+         # blocks (WHARF_N2V_LIST_ORDER=global; waves of entries from many blocks)
+         "sorted/global-move": ("sorted", "1", "0", "on", "1", "0", "on", "1", "0"),
          "block/slack": ("block", "0", "0", "on", "0", "0", "on", "0", "1"),
          "block/move-lazy": ("block", "1", "0", "noslack", "1", "0", "tiny", "1", "0"),
          "park/repack-tail": ("park", "1", "1", "off", "0", "1", "tiny", "0", "0"),
@@ -430,6 +433,7 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     monkeypatch.setenv("WHARF_NO_NEIGHBOUR_FILTER", "1" if filt == "off" else "0")
     monkeypatch.setenv("WHARF_FILTER_NO_SLACK", "1" if filt == "noslack" else "0")
     monkeypatch.setenv("WHARF_N2V_REWALK", n2v_list)
+    monkeypatch.setenv("WHARF_N2V_LIST_ORDER", "global" if path == "sorted/global-move" else "block")
     monkeypatch.setenv("WHARF_NO_ROW_SLACK", no_slack)
     monkeypatch.setenv("WHARF_POOL_NO_HEADROOM", no_headroom)
     base = O.generate_batch_of_edges(50000, 1 << 13, 6, False, False)
@@ -586,6 +590,28 @@ def test_walk_readout_snapshot_follows_every_change(W, monkeypatch):
     for j in (0, 17, len(ids) - 1):
         assert g.walk(int(ids[j])) == O.walk_string(w[j])
     g.destroy()
+
+
+def test_rewalk_list_entry_out_of_range_is_reported(W, monkeypatch):
+    """A node2vec re-walk list entry outside the walks (planted between the plan
+    and the consumer, WHARF_TEST_CORRUPT_LIST=1) is skipped, not dereferenced,
+    and the update fails with WHARF_E_STATE (round 3's global-sort fault:
+    k_rewalk_sorted read walks[p * W + li] for whatever the list held).  Every
+    list consumer: the lock-step sweep, the flat list, the passes."""
+    base = O.generate_batch_of_edges(20000, 1 << 12, 6, False, False)
+    off, adj = O.csr_from_edges(1 << 11, base)
+    b = O.generate_batch_of_edges(400, 1 << 11, 3, False, False)
+    for kernel in ("sorted", "flat", "park"):
+        monkeypatch.setenv("WHARF_N2V_REWALK", kernel)
+        cfg = W.WharfConfig(walks_per_vertex=4, walk_length=20, model=W.NODE2VEC, paramP=0.5, paramQ=2.0,
+                            deterministic=False, seed=5)
+        g = W.WharfMH.from_csr(off, adj, config=cfg)
+        g.generate_initial_random_walks()
+        monkeypatch.setenv("WHARF_TEST_CORRUPT_LIST", "1")
+        with pytest.raises(RuntimeError, match="outside the walks"):
+            g.insert_edges_batch(b, remove_dups=True)
+        monkeypatch.setenv("WHARF_TEST_CORRUPT_LIST", "0")
+        g.destroy()
 
 
 def test_walk_rows_export_and_sparse_readout(W):
