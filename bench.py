@@ -909,8 +909,13 @@ def main():
 
     if rank == 0:
         if rewalk and live_ceiling and bytes_per_step == BYTES_PER_STEP_DEEPWALK:
-            # re-walk steps (one gather each) against the same yardstick; the scan rides along
-            rewalk["rewalk_frac_of_gather_ceiling_min"] = round(rewalk["rewalk_Gsteps_per_s"] / min(live_ceiling), 4)
+            # re-walk steps (one gather each) against the same yardstick, with the probes' spread: the
+            # probe is a yardstick for the box, not a roof (a ratio above 1 is within its spread)
+            rewalk["rewalk_vs_gather_probes"] = {
+                "probe_Ggathers_per_s_min": round(min(live_ceiling), 2),
+                "probe_Ggathers_per_s_max": round(max(live_ceiling), 2),
+                "ratio_to_max_probe": round(rewalk["rewalk_Gsteps_per_s"] / max(live_ceiling), 4),
+                "ratio_to_min_probe": round(rewalk["rewalk_Gsteps_per_s"] / min(live_ceiling), 4)}
         achieved = (steps_local * bytes_per_step / (avg_kernel_ms * 1e-3) / 1e9) if bytes_per_step else None
         traffic, traffic_src = load_traffic(tag)
         line = {
