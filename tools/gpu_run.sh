@@ -10,6 +10,7 @@
 #                             BASELINE's 8-GPU jobs (configs[3], configs[4]) at scale - 4
 #   bigscale:<args>           tools/bigscale.py with args (',' for spaces)
 #   probe:<args>              tools/rewalk_probe.py with args (',' for spaces)
+#   exe:<cmd>                 a built probe, e.g. exe:tools/sort_probe (',' for spaces)
 #   prof                      rocprofv3 kernel trace + stats of a short default bench
 # Logs go to gpurun_out/<tag>_<step>.log; set TAG=... to name them.
 set -u
@@ -53,6 +54,9 @@ for step in "$@"; do
     probe)
         timeout -k 10 900 python -u tools/rewalk_probe.py $args > "$log" 2>&1
         rc=$?; tail -4 "$log" ;;
+    exe)
+        timeout -k 10 300 $args > "$log" 2>&1
+        rc=$?; tail -3 "$log" ;;
     prof)
         timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run -- \
             python3 bench.py --steps 5 --warmup 2 --rewalk-batches 10 --det-rewalk-batches 10 --n2v-steps 0 \
