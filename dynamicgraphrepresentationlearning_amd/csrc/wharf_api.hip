@@ -897,8 +897,8 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         h->walks_changed();
         HIPCHK(hipMemsetAsync(a.err, 0, 8, s));
         // node2vec list order (tests): WHARF_N2V_LIST_ORDER=global sorts k_rewalk_plan's list by
-        // rewalk point over all blocks (round 3's global sort, rebuilt: the count masked out of the
-        // packed word, the sort's output apart from rocPRIM's temp storage) before the consumer;
+        // rewalk point over all blocks (round 3's global sort, rebuilt on a full-width sort, below)
+        // before the consumer;
         // WHARF_TEST_CORRUPT_LIST=1 plants one out-of-range entry, which the consumer must report
         // (WHARF_E_STATE) without touching memory through it
         const char* lord = getenv("WHARF_N2V_LIST_ORDER");
@@ -918,7 +918,11 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
                 h->park.ensure(cnt * 8);
                 uint64_t* in = h->defer.as<uint64_t>();
                 uint64_t* out = h->park.as<uint64_t>();
-                h->rp([&](void* t, size_t& b) { return rocprim::radix_sort_keys(t, b, in, out, (size_t)cnt, 56u, 64u, s); });
+                // all 64 bits: by point, then walk.  NOT bits [56, 64) alone: rocPRIM's radix_sort_keys
+                // with begin_bit 56 returns a non-permutation for 3 k <= n <= 1 Mi keys in ROCm 7.2
+                // (tools/sort_probe, profiles/r04/sort_probe) — round 3's global sort fed those
+                // entries to k_rewalk_sorted, which dereferenced them
+                h->rp([&](void* t, size_t& b) { return rocprim::radix_sort_keys(t, b, in, out, (size_t)cnt, 0u, 64u, s); });
                 HIPCHK(hipMemcpyAsync(in, out, cnt * 8, hipMemcpyDeviceToDevice, s));
             }
             if (corrupt && cnt) {
