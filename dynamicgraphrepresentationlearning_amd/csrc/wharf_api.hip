@@ -903,8 +903,8 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         // (WHARF_E_STATE) without touching memory through it
         const char* lord = getenv("WHARF_N2V_LIST_ORDER");
         const char* lbad = getenv("WHARF_TEST_CORRUPT_LIST");
-        const bool n2v_list = a.model == kNode2Vec && !a.det && !a.scan_only && !a.park && !a.bdesc;
-        const bool gsort = n2v_list && lord && std::string(lord) == "global";
+        const bool n2v_list = a.model == kNode2Vec && !a.det && !a.scan_only && !a.bdesc;
+        const bool gsort = n2v_list && !a.park && lord && std::string(lord) == "global";
         const bool corrupt = n2v_list && lbad && atoi(lbad) != 0;
         if (gsort || corrupt) {
             a.stage = 1;

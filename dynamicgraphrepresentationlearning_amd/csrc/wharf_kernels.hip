@@ -1072,6 +1072,9 @@ __device__ __forceinline__ XcdRange xcd_range(uint64_t W)
 #ifndef WHARF_SCAN_ONLY_WAVES_EU
 #define WHARF_SCAN_ONLY_WAVES_EU 8
 #endif
+#ifndef WHARF_COPY_EARLY_ROWS
+#define WHARF_COPY_EARLY_ROWS 0   // A/B: the copy issues the next chunk's rows before its source-index wait
+#endif
 #ifndef WHARF_COPY_WAVES
 #define WHARF_COPY_WAVES 1   // A/B: minimum waves/SIMD of the copy (1 = the compiler's choice; the 32-KiB
                              // filter caps it at 5 by LDS; 16-KiB filter forced to 6: 100 B spilled, 16 vs
@@ -1106,7 +1109,7 @@ __global__ __launch_bounds__(256, COPY ? WHARF_COPY_WAVES : WHARF_SCAN_ONLY_WAVE
             const bool more = c0 + C < L;
             ChunkTest ct;
             if (scanning) chunk_issue<FB, WHARF_CHUNK_LEAN != 0, COPY && IDX>(a, s_bloom, cur, cnt, ct);
-            if (!COPY && more && scanning) {
+            if ((!COPY || WHARF_COPY_EARLY_ROWS) && more && scanning) {
                 // scan only: the next chunk's rows go out before the bitmap words
                 // are waited for (loads complete in order: the wait leaves them in flight)
 #pragma unroll
@@ -1140,7 +1143,7 @@ __global__ __launch_bounds__(256, COPY ? WHARF_COPY_WAVES : WHARF_SCAN_ONLY_WAVE
                 }
             }
             // next chunk's rows, in flight while this chunk is written
-            if (COPY && more && scanning) {
+            if (COPY && !WHARF_COPY_EARLY_ROWS && more && scanning) {
 #pragma unroll
                 for (uint32_t j = 0; j < C; j++)
                     nxt[j] = c0 + C + j < L ? row_load<NTL>(wb + (uint64_t)(c0 + C + j) * W, lane) : kSent;

@@ -11,6 +11,9 @@
 #   bigscale:<args>           tools/bigscale.py with args (',' for spaces)
 #   probe:<args>              tools/rewalk_probe.py with args (',' for spaces)
 #   exe:<cmd>                 a built probe, e.g. exe:tools/sort_probe (',' for spaces)
+#   rocprof:<script args>     rocprofv3 --kernel-trace --stats of python3 <script args> (',' for spaces)
+#   ab:<names>                tools/rewalk_probe.py $PROBE_ARGS with tools/ab/lib_<name>.so per name
+#                             ('base' = the tree's library), alternated twice
 #   prof                      rocprofv3 kernel trace + stats of a short default bench
 # Logs go to gpurun_out/<tag>_<step>.log; set TAG=... to name them.
 set -u
@@ -57,6 +60,19 @@ for step in "$@"; do
     exe)
         timeout -k 10 300 $args > "$log" 2>&1
         rc=$?; tail -3 "$log" ;;
+    rocprof)   # rocprof:<python script and args>: kernel trace + stats of that run
+        timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run -- python3 $args > "$log" 2>&1
+        rc=$?; tail -2 "$log" ;;
+    ab)   # ab:<lib1>,<lib2>,...: tools/rewalk_probe.py with each tools/ab/lib_<name>.so (base = the tree's), twice
+        for rep in 1 2; do
+            for lib in $args; do
+                if [ "$lib" = base ]; then unset WHARF_LIB_PATH; else export WHARF_LIB_PATH=tools/ab/lib_$lib.so; fi
+                timeout -k 10 600 python -u tools/rewalk_probe.py $PROBE_ARGS > gpurun_out/${TAG}_ab_${lib}_$rep.log 2>&1
+                rc=$?; echo "$lib rep $rep: $(tail -1 gpurun_out/${TAG}_ab_${lib}_$rep.log)"
+                [ $rc -eq 0 ] || exit $rc
+            done
+        done
+        unset WHARF_LIB_PATH ;;
     prof)
         timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run -- \
             python3 bench.py --steps 5 --warmup 2 --rewalk-batches 10 --det-rewalk-batches 10 --n2v-steps 0 \
