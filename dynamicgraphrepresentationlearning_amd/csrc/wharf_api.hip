@@ -107,6 +107,7 @@ struct wharf_handle {
     DevBuf preoff;                             // node2vec MH: per-source degree prefix of the anchor pre-init
     DevBuf stab;                               // node2vec MH re-walk: start-state anchor table (k_rewalk_sorted)
     DevBuf sanc;                               // anchor carry: the sources' old anchor entries (k_save_rows)
+    DevBuf rchunk;                             // per batch source: chunk counts, then their exclusive prefix (k_*_rows_c)
     bool symmetric = false;                    // every edge's reverse is an edge (anchor carry needs it)
     DevBuf park, parkc;                        // node2vec MH re-walk passes: two parked-walker lists, their counts
     DevBuf bdesc;                              // node2vec MH block re-walk: per 256-walk block, its run of the list
@@ -558,7 +559,8 @@ struct wharf_handle {
             build_filters();   // out of headroom: re-size and re-fill every row (drops the gaps)
             return;
         }
-        launch_filter_rows(runs_d, k, off.as<uint64_t>(), deg.as<uint32_t>(), adj.as<uint32_t>(), need, gofs, fpool_used,
+        launch_filter_rows(runs_d, k, rchunk.as<uint32_t>() + (k + 1), off.as<uint64_t>(), deg.as<uint32_t>(),
+                           adj.as<uint32_t>(), need, gofs, fpool_used,
                            fdir.as<uint64_t>(), fpool.as<uint32_t>(), s);
         fpool_used += grow;
     }
@@ -711,7 +713,7 @@ void free_handle(wharf_handle* h)
                       &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->walks, &h->aff, &h->rtab,
                       &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags, &h->chg, &h->cf,
                       &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel, &h->defer, &h->rplan, &h->pscan,
-                      &h->scratch, &h->stab, &h->preoff, &h->park, &h->parkc, &h->bdesc, &h->sanc})
+                      &h->scratch, &h->stab, &h->preoff, &h->park, &h->parkc, &h->bdesc, &h->sanc, &h->rchunk})
         b->release();
     h->free_snaps();
     for (auto& e : h->ev)
@@ -1106,9 +1108,17 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->scratch.ensure(std::max<uint64_t>(saved, 1) * 4);
         h->start_bound = saved + (insert ? total_chg : 0);   // the sources' degrees after the update, at most
         const uint32_t rs = (uint32_t)h->rec_stride();
-        launch_save_rows(h->runs.as<RunInfo>(), k, h->adj.as<uint32_t>(), sofs, h->scratch.as<uint32_t>(), anc_base,
+        // source rows in chunks: counts of each run's longest range, exclusive prefix (k_run_chunks)
+        h->rchunk.ensure((k + 1) * 8);
+        uint32_t* rcnt = h->rchunk.as<uint32_t>();
+        uint32_t* rpre = rcnt + (k + 1);
+        launch_run_chunks(h->runs.as<RunInfo>(), h->rplan.as<RowPlan>(), k, rcnt, s);
+        h->rp([&](void* t, size_t& b) {
+            return rocprim::exclusive_scan(t, b, rcnt, rpre, 0u, (size_t)(k + 1), rocprim::plus<uint32_t>(), s);
+        });
+        launch_save_rows(h->runs.as<RunInfo>(), k, rpre, h->adj.as<uint32_t>(), sofs, h->scratch.as<uint32_t>(), anc_base,
                          carry ? h->sanc.as<uint64_t>() : nullptr, s);
-        launch_merge_rows(h->runs.as<RunInfo>(), k, bkeys, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(),
+        launch_merge_rows(h->runs.as<RunInfo>(), k, rpre, bkeys, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(),
                           h->scratch.as<uint32_t>(), sofs, relofs, h->pool_used, insert, h->rplan.as<RowPlan>(),
                           h->adj.as<uint32_t>(), carry ? h->sanc.as<uint64_t>() : nullptr, anc_base, s);
         launch_commit_rows(h->runs.as<RunInfo>(), k, h->rplan.as<RowPlan>(), h->epoch, h->off.as<uint64_t>(),
@@ -1117,7 +1127,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->m = m_new;
         // records: the source rows' slots (anchors reset), then every slot whose
         // target is a source (one streaming scan of the pool)
-        launch_erec_rows(h->runs.as<RunInfo>(), k, h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->adj.as<uint32_t>(),
+        launch_erec_rows(h->runs.as<RunInfo>(), k, rpre, h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->adj.as<uint32_t>(),
                          h->vrec.as<ERec>(), h->erec.as<ERec>(), rs, carry ? 1 : 0, s);
         HIPCHK(hipEventRecord(h->ev[4], s));
         launch_patch_in_edges(h->adj.as<uint32_t>(), h->pool_used, h->bitmap.as<uint32_t>(),
@@ -1794,7 +1804,7 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
                       h->runs.cap + h->fplan.cap + h->memo.cap + h->srcidx.cap + h->count.cap + h->pairs.cap +
                       h->sel.cap + h->defer.cap + h->park.cap + h->parkc.cap + h->stab.cap + h->preoff.cap + h->rtab.cap + h->bitmap.cap + h->counters.cap +
-                      h->errflag.cap + h->bdesc.cap;
+                      h->errflag.cap + h->bdesc.cap + h->rchunk.cap;
     r.total_bytes = r.csr_bytes + r.records_bytes + r.walks_bytes + r.samplers_bytes + r.edge_hash_bytes +
                     r.update_buffers_bytes + r.scratch_bytes;
     *out = r;

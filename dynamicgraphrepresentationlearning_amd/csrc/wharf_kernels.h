@@ -125,19 +125,22 @@ void launch_compact_gather(const uint32_t* order, const uint64_t* snoff, uint64_
 void launch_compact_put(const uint32_t* sadj, const uint64_t* sanc, uint64_t cnt, uint64_t D, uint32_t* adj,
                         uint64_t* anc, hipStream_t s);
 void launch_scatter_offsets(const uint32_t* order, const uint64_t* snoff, uint64_t n, uint64_t* off, hipStream_t s);
-void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* adj, const uint64_t* sofs, uint32_t* scratch,
-                      const uint64_t* anc, uint64_t* sanc, hipStream_t s);
-void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint64_t* bkeys, const uint32_t* chg, const uint32_t* cf,
-                       const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs, uint64_t pool_end,
-                       int insert, RowPlan* plan, uint32_t* adj, const uint64_t* sanc, uint64_t* anc, hipStream_t s);
+// source rows in chunks (`pre`: exclusive prefix of launch_run_chunks' counts; null: a workgroup per row)
+void launch_run_chunks(const RunInfo* runs, const RowPlan* plan, uint64_t k, uint32_t* cnt, hipStream_t s);
+void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint32_t* adj, const uint64_t* sofs,
+                      uint32_t* scratch, const uint64_t* anc, uint64_t* sanc, hipStream_t s);
+void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* bkeys, const uint32_t* chg,
+                       const uint32_t* cf, const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs,
+                       uint64_t pool_end, int insert, RowPlan* plan, uint32_t* adj, const uint64_t* sanc, uint64_t* anc,
+                       hipStream_t s);
 void launch_anchor_invalidate(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint64_t* off,
                               const uint32_t* deg, const uint32_t* adj, uint64_t* anc, const uint64_t* fdir,
                               const uint32_t* fpool, hipStream_t s);
 void launch_keys_symmetric(const uint64_t* keys, uint64_t m, unsigned long long* asym, hipStream_t s);
 void launch_commit_rows(const RunInfo* runs, uint64_t k, const RowPlan* plan, uint32_t epoch, uint64_t* off,
                         uint32_t* deg, uint32_t* cap, ERec* vrec, uint32_t* row_epoch, hipStream_t s);
-void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* off, const uint32_t* deg, const uint32_t* adj,
-                      const ERec* vrec, ERec* erec, uint32_t rs, int keep_anc, hipStream_t s);
+void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* off, const uint32_t* deg,
+                      const uint32_t* adj, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anc, hipStream_t s);
 void launch_patch_in_edges(const uint32_t* adj, uint64_t slots, const uint32_t* bitmap, const uint32_t* bloom,
                            const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s);
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s);
@@ -168,9 +171,9 @@ void launch_filter_fill(const uint64_t* off, const uint32_t* deg, uint64_t n, co
                         uint32_t* pool, hipStream_t s);
 void launch_filter_plan(const RunInfo* runs, uint64_t k, const uint32_t* deg, const uint64_t* fdir, uint64_t* need,
                         hipStream_t s);
-void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* deg, const uint32_t* adj,
-                        const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir, uint32_t* pool,
-                        hipStream_t s);
+void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* noff, const uint32_t* deg,
+                        const uint32_t* adj, const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir,
+                        uint32_t* pool, hipStream_t s);
 void launch_szudzik64(int op, uint64_t cnt, uint64_t* x, uint64_t* y, uint64_t* z, hipStream_t s);
 
 }  // namespace wharf

@@ -2209,12 +2209,6 @@ void launch_filter_plan(const RunInfo* runs, uint64_t k, const uint32_t* deg, co
     hipLaunchKernelGGL(k_filter_plan, grid_for(k + 1, 256), 256, 0, s, runs, k, deg, fdir, need);
 }
 
-void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint64_t* noff, const uint32_t* deg, const uint32_t* adj,
-                        const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir, uint32_t* pool,
-                        hipStream_t s)
-{
-    if (k) hipLaunchKernelGGL(k_filter_rows, (unsigned)k, 256, 0, s, runs, noff, deg, adj, need, gofs, base, fdir, pool);
-}
 
 __global__ void k_csr_to_keys(const uint64_t* __restrict__ off, uint64_t n, const uint32_t* __restrict__ tgt,
                               uint64_t* __restrict__ keys, unsigned long long* __restrict__ err)
@@ -2533,6 +2527,189 @@ __global__ void k_merge_rows(const RunInfo* __restrict__ runs, const uint64_t* _
     __syncthreads();   // every thread has read plan[j] before it is resolved
     if (threadIdx.x == 0) plan[j].noff = noff;
 }
+
+// ---------------------------------------------------------------------------
+// Source rows in chunks (round 4).  The kernels above take one workgroup per
+// batch source; a hub source's row (10^5-10^6 slots on the configs[3] / [4]
+// graphs) then runs on one CU while the rest of the chip idles: in the
+// configs[4] shard's update, save / merge / records / filters took 0.6 / 0.7 /
+// 0.76 / 1.47 ms, nearly all of it the few hub rows' workgroups
+// (profiles/r04/update_rows).  Here every run is cut into kRowChunk-slot
+// chunks of its longest range (old row, old and new capacity), the chunk counts
+// are prefix-summed on the device, and a persistent grid deals the chunks, so a
+// hub row spreads over the chip.  Every element's work is independent (the
+// merge reads the saved copy of the old row, so its writes may land in any
+// order), and the one write that ordered them — the move target resolved into
+// plan[j].noff at the end of k_merge_rows — is a separate kernel after it.
+// ---------------------------------------------------------------------------
+#ifndef WHARF_ROW_CHUNKED
+#define WHARF_ROW_CHUNKED 1   // A/B: 0 = a workgroup per source row (round 3)
+#endif
+constexpr uint32_t kRowChunk = 4096;
+
+__global__ void k_run_chunks(const RunInfo* __restrict__ runs, const RowPlan* __restrict__ plan, uint64_t k,
+                             uint32_t* __restrict__ cnt)
+{
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= k; j += (uint64_t)gridDim.x * blockDim.x) {
+        if (j == k) { cnt[k] = 0; continue; }
+        const uint64_t d = runs[j].end - runs[j].off;
+        const uint64_t len = max(max(d, (uint64_t)plan[j].ocap), max((uint64_t)plan[j].ncap, (uint64_t)1));
+        cnt[j] = (uint32_t)((len + kRowChunk - 1) / kRowChunk);
+    }
+}
+
+// chunk t of the prefix `pre` (pre[k] = total): its run j and the run's chunk c
+__device__ __forceinline__ bool run_chunk(const uint32_t* __restrict__ pre, uint64_t k, uint64_t t, uint64_t& j,
+                                          uint32_t& c)
+{
+    if (t >= pre[k]) return false;
+    uint64_t lo = 0, hi = k;   // the last run with pre[run] <= t
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= t) lo = mid; else hi = mid;
+    }
+    j = lo;
+    c = (uint32_t)(t - pre[lo]);
+    return true;
+}
+
+__global__ void k_save_rows_c(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
+                              const uint32_t* __restrict__ adj, const uint64_t* __restrict__ sofs,
+                              uint32_t* __restrict__ scratch, const uint64_t* __restrict__ anc, uint64_t* __restrict__ sanc)
+{
+    for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
+        uint64_t j;
+        uint32_t c;
+        if (!run_chunk(pre, k, t, j, c)) break;
+        const uint64_t lo = (uint64_t)c * kRowChunk;
+        const RunInfo ri = runs[j];
+        const uint64_t d = ri.end - ri.off, hi = min(d, lo + kRowChunk);
+        uint32_t* __restrict__ out = scratch + sofs[j];
+        for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+            out[i] = adj[ri.off + i];
+            if (sanc) sanc[sofs[j] + i] = anc[(ri.off + i) * kAnchorStride];
+        }
+    }
+}
+
+__global__ void k_merge_rows_c(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
+                               const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ chg,
+                               const uint32_t* __restrict__ cf, const uint32_t* __restrict__ scratch,
+                               const uint64_t* __restrict__ sofs, const uint64_t* __restrict__ relofs, uint64_t pool_end,
+                               int insert, const RowPlan* __restrict__ plan, uint32_t* __restrict__ adj,
+                               const uint64_t* __restrict__ sanc, uint64_t* __restrict__ anc)
+{
+    for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
+        uint64_t j;
+        uint32_t c;
+        if (!run_chunk(pre, k, t, j, c)) break;
+        const uint64_t lo = (uint64_t)c * kRowChunk;
+        const RunInfo ri = runs[j];
+        const RowPlan p = plan[j];   // (noff is resolved by k_resolve_plan, after every chunk)
+        const bool reloc = p.noff == kRelocate;
+        const uint64_t noff = reloc ? pool_end + relofs[j] : ri.off;
+        const uint32_t d = (uint32_t)(ri.end - ri.off), nb = ri.re - ri.rs, base = cf[ri.rs];
+        const uint32_t* __restrict__ old = scratch + sofs[j];
+        const uint64_t* __restrict__ bk = bkeys + ri.rs;
+        const uint64_t hi = lo + kRowChunk;
+        for (uint64_t i = lo + threadIdx.x; i < min(hi, (uint64_t)d); i += blockDim.x) {
+            const uint32_t x = old[i];
+            const uint32_t lb = lower_bound_dst(bk, nb, x);
+            const uint32_t below = cf[ri.rs + lb] - base;
+            uint64_t at = ~0ull;
+            if (insert) at = noff + i + below;
+            else if (!(lb < nb && (uint32_t)bk[lb] == x && chg[ri.rs + lb])) at = noff + i - below;
+            if (at != ~0ull) {
+                adj[at] = x;
+                if (sanc) anc[at * kAnchorStride] = sanc[sofs[j] + i];   // the entry travels with its edge
+            }
+        }
+        if (insert && c == 0) {
+            for (uint32_t e = threadIdx.x; e < nb; e += blockDim.x) {
+                if (!chg[ri.rs + e]) continue;
+                const uint32_t x = (uint32_t)bk[e];
+                const uint64_t at = noff + (cf[ri.rs + e] - base) + lower_bound_u32(old, d, x);
+                adj[at] = x;
+                if (sanc) anc[at * kAnchorStride] = kAnchorNone64;
+            }
+        }
+        if (reloc) {
+            for (uint64_t i = lo + threadIdx.x; i < min(hi, (uint64_t)p.ocap); i += blockDim.x) adj[ri.off + i] = kGap;
+            for (uint64_t i = max(lo, (uint64_t)p.ndeg) + threadIdx.x; i < min(hi, (uint64_t)p.ncap); i += blockDim.x)
+                adj[noff + i] = kGap;
+        } else {
+            for (uint64_t i = max(lo, (uint64_t)p.ndeg) + threadIdx.x; i < min(hi, (uint64_t)d); i += blockDim.x)
+                adj[ri.off + i] = kGap;
+        }
+    }
+}
+
+__global__ void k_resolve_plan(const RunInfo* __restrict__ runs, uint64_t k, const uint64_t* __restrict__ relofs,
+                               uint64_t pool_end, RowPlan* __restrict__ plan)
+{
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += (uint64_t)gridDim.x * blockDim.x)
+        plan[j].noff = plan[j].noff == kRelocate ? pool_end + relofs[j] : runs[j].off;
+}
+
+__global__ void k_erec_rows_c(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
+                              const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg,
+                              const uint32_t* __restrict__ adj, const ERec* __restrict__ vrec, ERec* __restrict__ erec,
+                              uint32_t rs, int keep_anc)
+{
+    for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
+        uint64_t j;
+        uint32_t c;
+        if (!run_chunk(pre, k, t, j, c)) break;
+        const uint64_t lo = (uint64_t)c * kRowChunk;
+        const uint32_t s = runs[j].src;
+        const uint64_t b = off[s], e = b + deg[s];
+        for (uint64_t q = b + lo + threadIdx.x; q < min(e, b + lo + kRowChunk); q += blockDim.x) {
+            erec[q * rs] = vrec[adj[q]];
+            if (rs == 2 && !keep_anc) reinterpret_cast<uint64_t*>(erec)[q * kAnchorStride + 2] = kAnchorNone64;
+        }
+    }
+}
+
+// per batch source: its neighbour filter's new descriptor (rows that outgrew their words)
+__global__ void k_filter_desc(const RunInfo* __restrict__ runs, uint64_t k, const uint32_t* __restrict__ deg,
+                              const uint64_t* __restrict__ need, const uint64_t* __restrict__ gofs, uint64_t base,
+                              uint64_t* __restrict__ fdir)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < k; i += (uint64_t)gridDim.x * blockDim.x)
+        if (need[i]) fdir[runs[i].src] = (base + gofs[i]) | ((uint64_t)filt_log2_words(deg[runs[i].src]) << kFiltOffBits);
+}
+
+__global__ void k_filter_clear_c(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
+                                 const uint64_t* __restrict__ fdir, uint32_t* __restrict__ pool)
+{
+    for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
+        uint64_t j;
+        uint32_t c;
+        if (!run_chunk(pre, k, t, j, c)) break;
+        const uint64_t lo = (uint64_t)c * kRowChunk;
+        const uint64_t fd = fdir[runs[j].src], w0 = fd & kFiltOffMask, nw = 1ull << (fd >> kFiltOffBits);
+        for (uint64_t q = lo + threadIdx.x; q < min(nw, lo + kRowChunk); q += blockDim.x) pool[w0 + q] = 0;
+    }
+}
+
+__global__ void k_filter_fill_c(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
+                                const uint64_t* __restrict__ noff, const uint32_t* __restrict__ deg,
+                                const uint32_t* __restrict__ adj, const uint64_t* __restrict__ fdir,
+                                uint32_t* __restrict__ pool)
+{
+    for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
+        uint64_t j;
+        uint32_t c;
+        if (!run_chunk(pre, k, t, j, c)) break;
+        const uint64_t lo = (uint64_t)c * kRowChunk;
+        const uint32_t u = runs[j].src;
+        const uint64_t fd = fdir[u], b = noff[u];
+        for (uint64_t q = lo + threadIdx.x; q < min((uint64_t)deg[u], lo + kRowChunk); q += blockDim.x)
+            filter_set(pool, fd, adj[b + q]);
+    }
+}
+
+static unsigned chunk_grid() { return cu_count() * 4; }
 
 // per run: the source's new row and record, and its row epoch: the source's
 // samplers are reset (wharfmh.h:504,539).  Runs after the last point where the
@@ -3045,15 +3222,33 @@ void launch_compact_put(const uint32_t* sadj, const uint64_t* sanc, uint64_t cnt
 { if (cnt) hipLaunchKernelGGL(k_compact_put, grid_for(cnt, 256), 256, 0, s, sadj, sanc, cnt, D, adj, anc); }
 void launch_scatter_offsets(const uint32_t* order, const uint64_t* snoff, uint64_t n, uint64_t* off, hipStream_t s)
 { hipLaunchKernelGGL(k_scatter_offsets, grid_for(n + 1, 256), 256, 0, s, order, snoff, n, off); }
-void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* adj, const uint64_t* sofs, uint32_t* scratch,
-                      const uint64_t* anc, uint64_t* sanc, hipStream_t s)
-{ if (k) hipLaunchKernelGGL(k_save_rows, (unsigned)k, 256, 0, s, runs, adj, sofs, scratch, anc, sanc); }
-void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint64_t* bkeys, const uint32_t* chg, const uint32_t* cf,
-                       const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs, uint64_t pool_end,
-                       int insert, RowPlan* plan, uint32_t* adj, const uint64_t* sanc, uint64_t* anc, hipStream_t s)
+void launch_run_chunks(const RunInfo* runs, const RowPlan* plan, uint64_t k, uint32_t* cnt, hipStream_t s)
 {
-    if (k) hipLaunchKernelGGL(k_merge_rows, (unsigned)k, 256, 0, s, runs, bkeys, chg, cf, scratch, sofs, relofs,
-                              pool_end, insert, plan, adj, sanc, anc);
+    hipLaunchKernelGGL(k_run_chunks, grid_for(k + 1, 256), 256, 0, s, runs, plan, k, cnt);
+}
+void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint32_t* adj, const uint64_t* sofs,
+                      uint32_t* scratch, const uint64_t* anc, uint64_t* sanc, hipStream_t s)
+{
+    if (!k) return;
+    if (WHARF_ROW_CHUNKED && pre)
+        hipLaunchKernelGGL(k_save_rows_c, chunk_grid(), 256, 0, s, runs, pre, k, adj, sofs, scratch, anc, sanc);
+    else
+        hipLaunchKernelGGL(k_save_rows, (unsigned)k, 256, 0, s, runs, adj, sofs, scratch, anc, sanc);
+}
+void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* bkeys, const uint32_t* chg,
+                       const uint32_t* cf, const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs,
+                       uint64_t pool_end, int insert, RowPlan* plan, uint32_t* adj, const uint64_t* sanc, uint64_t* anc,
+                       hipStream_t s)
+{
+    if (!k) return;
+    if (WHARF_ROW_CHUNKED && pre) {
+        hipLaunchKernelGGL(k_merge_rows_c, chunk_grid(), 256, 0, s, runs, pre, k, bkeys, chg, cf, scratch, sofs, relofs,
+                           pool_end, insert, plan, adj, sanc, anc);
+        hipLaunchKernelGGL(k_resolve_plan, grid_for(k, 256), 256, 0, s, runs, k, relofs, pool_end, plan);
+    } else {
+        hipLaunchKernelGGL(k_merge_rows, (unsigned)k, 256, 0, s, runs, bkeys, chg, cf, scratch, sofs, relofs,
+                           pool_end, insert, plan, adj, sanc, anc);
+    }
 }
 void launch_anchor_invalidate(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint64_t* off,
                               const uint32_t* deg, const uint32_t* adj, uint64_t* anc, const uint64_t* fdir,
@@ -3067,9 +3262,28 @@ void launch_keys_symmetric(const uint64_t* keys, uint64_t m, unsigned long long*
 void launch_commit_rows(const RunInfo* runs, uint64_t k, const RowPlan* plan, uint32_t epoch, uint64_t* off,
                         uint32_t* deg, uint32_t* cap, ERec* vrec, uint32_t* row_epoch, hipStream_t s)
 { if (k) hipLaunchKernelGGL(k_commit_rows, grid_for(k, 256), 256, 0, s, runs, k, plan, epoch, off, deg, cap, vrec, row_epoch); }
-void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint64_t* off, const uint32_t* deg, const uint32_t* adj,
-                      const ERec* vrec, ERec* erec, uint32_t rs, int keep_anc, hipStream_t s)
-{ if (k) hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, off, deg, adj, vrec, erec, rs, keep_anc); }
+void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* off, const uint32_t* deg,
+                      const uint32_t* adj, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anc, hipStream_t s)
+{
+    if (!k) return;
+    if (WHARF_ROW_CHUNKED && pre)
+        hipLaunchKernelGGL(k_erec_rows_c, chunk_grid(), 256, 0, s, runs, pre, k, off, deg, adj, vrec, erec, rs, keep_anc);
+    else
+        hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, off, deg, adj, vrec, erec, rs, keep_anc);
+}
+void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* noff, const uint32_t* deg,
+                        const uint32_t* adj, const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir,
+                        uint32_t* pool, hipStream_t s)
+{
+    if (!k) return;
+    if (WHARF_ROW_CHUNKED && pre) {   // descriptors, then every row's words cleared, then filled
+        hipLaunchKernelGGL(k_filter_desc, grid_for(k, 256), 256, 0, s, runs, k, deg, need, gofs, base, fdir);
+        hipLaunchKernelGGL(k_filter_clear_c, chunk_grid(), 256, 0, s, runs, pre, k, fdir, pool);
+        hipLaunchKernelGGL(k_filter_fill_c, chunk_grid(), 256, 0, s, runs, pre, k, noff, deg, adj, fdir, pool);
+    } else {
+        hipLaunchKernelGGL(k_filter_rows, (unsigned)k, 256, 0, s, runs, noff, deg, adj, need, gofs, base, fdir, pool);
+    }
+}
 void launch_patch_in_edges(const uint32_t* adj, uint64_t slots, const uint32_t* bitmap, const uint32_t* bloom,
                            const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s)
 {

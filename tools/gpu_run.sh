@@ -12,8 +12,8 @@
 #   probe:<args>              tools/rewalk_probe.py with args (',' for spaces)
 #   exe:<cmd>                 a built probe, e.g. exe:tools/sort_probe (',' for spaces)
 #   rocprof:<script args>     rocprofv3 --kernel-trace --stats of python3 <script args> (',' for spaces)
-#   ab:<names>                tools/rewalk_probe.py $PROBE_ARGS with tools/ab/lib_<name>.so per name
-#                             ('base' = the tree's library), alternated twice
+#   ab:<names>                ${AB_SCRIPT:-tools/rewalk_probe.py} $PROBE_ARGS with tools/ab/lib_<name>.so per
+#                             name ('base' = the tree's library), alternated twice
 #   prof                      rocprofv3 kernel trace + stats of a short default bench
 # Logs go to gpurun_out/<tag>_<step>.log; set TAG=... to name them.
 set -u
@@ -67,7 +67,7 @@ for step in "$@"; do
         for rep in 1 2; do
             for lib in $args; do
                 if [ "$lib" = base ]; then unset WHARF_LIB_PATH; else export WHARF_LIB_PATH=tools/ab/lib_$lib.so; fi
-                timeout -k 10 600 python -u tools/rewalk_probe.py $PROBE_ARGS > gpurun_out/${TAG}_ab_${lib}_$rep.log 2>&1
+                timeout -k 10 600 python -u ${AB_SCRIPT:-tools/rewalk_probe.py} $PROBE_ARGS > gpurun_out/${TAG}_ab_${lib}_$rep.log 2>&1
                 rc=$?; echo "$lib rep $rep: $(tail -1 gpurun_out/${TAG}_ab_${lib}_$rep.log)"
                 [ $rc -eq 0 ] || exit $rc
             done
