@@ -1997,7 +1997,10 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
         // the 32-KiB filter (5 workgroups of 256 per CU still fit the 160 KiB of LDS);
         // WHARF_COPY_SMALL_BLOOM=1 (A/B): the 16-KiB one
         const char* cb = getenv("WHARF_COPY_SMALL_BLOOM");
-        if (cb && atoi(cb)) {
+        if (cb && atoi(cb) && a.src_exact) {
+            if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<true, true, 0, true>), mgrid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_rewalk_chunked<true, false, 0, true>), mgrid, block, 0, s, a);
+        } else if (cb && atoi(cb)) {
             if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_chunked<true, true, 0>), mgrid, block, 0, s, a);
             else hipLaunchKernelGGL((k_rewalk_chunked<true, false, 0>), mgrid, block, 0, s, a);
         } else if (a.src_exact) {   // the source index settles the positives (IDX)

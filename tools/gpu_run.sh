@@ -65,10 +65,13 @@ for step in "$@"; do
         rc=$?; tail -2 "$log" ;;
     ab)   # ab:<lib1>,<lib2>,...: tools/rewalk_probe.py with each tools/ab/lib_<name>.so (base = the tree's), twice
         for rep in 1 2; do
-            for lib in $args; do
+            for item in $args; do   # <lib>[@VAR=value]: the variant's library and one environment setting
+                lib=${item%%@*}; envset=""; [ "$lib" != "$item" ] && envset=${item#*@}
                 if [ "$lib" = base ]; then unset WHARF_LIB_PATH; else export WHARF_LIB_PATH=tools/ab/lib_$lib.so; fi
-                timeout -k 10 600 python -u ${AB_SCRIPT:-tools/rewalk_probe.py} $PROBE_ARGS > gpurun_out/${TAG}_ab_${lib}_$rep.log 2>&1
-                rc=$?; echo "$lib rep $rep: $(tail -1 gpurun_out/${TAG}_ab_${lib}_$rep.log)"
+                tag=${item//[@=]/_}
+                ( [ -n "$envset" ] && export "$envset"; timeout -k 10 600 python -u ${AB_SCRIPT:-tools/rewalk_probe.py} $PROBE_ARGS ) \
+                    > gpurun_out/${TAG}_ab_${tag}_$rep.log 2>&1
+                rc=$?; echo "$item rep $rep: $(tail -1 gpurun_out/${TAG}_ab_${tag}_$rep.log)"
                 [ $rc -eq 0 ] || exit $rc
             done
         done
