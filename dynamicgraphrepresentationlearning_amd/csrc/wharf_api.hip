@@ -173,7 +173,9 @@ struct wharf_handle {
         }
         if (snap_of[c] >= 0) return snaps[snap_of[c]].host + (li - c * kSnapWalks) * L;
         if (one_version == walks_version && one_li == li) return one_row.data();
-        if (snap_reads[c] < kSnapFillAfter) {   // sparse so far: this row alone
+        const char* fa = getenv("WHARF_WALK_FILL_AFTER");   // A/B (tools/walk_readout): 0 = round 3's rule
+        const uint32_t fill_after = fa && *fa ? (uint32_t)atoi(fa) : kSnapFillAfter;
+        if (snap_reads[c] < fill_after) {   // sparse so far: this row alone
             snap_reads[c]++;
             one_row.resize(L);
             sel.ensure(L * 4);

@@ -3,6 +3,12 @@
 // Times wharf_walk_string over the first `n_old` walks with a device read per call
 // (WHARF_WALK_NO_SNAPSHOT=1, round 2's path) and over the first `n_new` walks through
 // the host snapshot, on configs[1]'s graph (RMAT scale 22, 117 M samples, wpv 10, L 80).
+// Then the reference's incremental pattern (vertex-classification.cpp:171-176):
+// after each insert batch of the throughput driver's sizes (5 / 50 / 500
+// directed edges, throughput-latency.cpp:87-93,121), walk(i) of the affected
+// walks only — with the snapshot chunk taken once 32 of its walks were read
+// (default), taken on the first read (WHARF_WALK_FILL_AFTER=0, round 3), and a
+// device read per call.
 //
 //   tools/walk_readout [n_old=20000] [n_new=41943040]
 #include <chrono>
@@ -47,11 +53,45 @@ int main(int argc, char** argv)
         total += len;
     }
     const double t_new = now() - t0;
+    // sparse: the affected walks of small batches
+    std::vector<uint32_t> aff(W), pairs;
+    std::string sparse = "[";
+    for (uint64_t bs : {5ull, 50ull, 500ull}) {
+        pairs.assign(2 * bs, 0);
+        uint64_t cnt = 0, naff = 0;
+        if (wharf_generate_batch_of_edges(0, bs, n, 1000 + bs, 0, 1, 0.5, 0.2, 0.1, pairs.data(), &cnt) ||
+            wharf_insert_edges(h, cnt, pairs.data(), WHARF_REMOVE_DUPS | WHARF_APPLY_WALK_UPDATES, aff.data(), &naff))
+            return 4;
+        const char* modes[3][2] = {{"fill_after_32", nullptr}, {"fill_on_first_read", "0"}, {"device_read_per_call", nullptr}};
+        std::string rec = "{\"batch_edges\": " + std::to_string(cnt) + ", \"affected\": " + std::to_string(naff);
+        for (int m = 0; m < 3; m++) {
+            // a fresh snapshot per mode: one tiny update that changes no walk would not invalidate it,
+            // so re-set the walks' version through the library's own rule (an empty walk update)
+            uint32_t none = 0;
+            uint64_t dummy = 0;
+            if (wharf_batch_walk_update(h, &none, 0, 0, nullptr, &dummy)) return 5;
+            if (m == 1) setenv("WHARF_WALK_FILL_AFTER", "0", 1);
+            if (m == 2) setenv("WHARF_WALK_NO_SNAPSHOT", "1", 1);
+            t0 = now();
+            for (uint64_t i = 0; i < naff; i++) {
+                if (wharf_walk_string(h, aff[i], buf.data(), buf.size(), &len)) return 6;
+                total += len;
+            }
+            const double t = now() - t0;
+            unsetenv("WHARF_WALK_NO_SNAPSHOT");
+            char part[160];
+            snprintf(part, sizeof part, ", \"%s_ms\": %.3f", modes[m][0], 1e3 * t);
+            rec += part;
+        }
+        sparse += (sparse.size() > 1 ? ", " : "") + rec + "}";
+        unsetenv("WHARF_WALK_FILL_AFTER");
+    }
+    sparse += "]";
     printf("{\"walks\": %llu, \"per_call_device_read\": {\"calls\": %llu, \"seconds\": %.3f, \"us_per_call\": %.2f, "
            "\"all_walks_seconds_extrapolated\": %.1f}, \"host_snapshot\": {\"calls\": %llu, \"seconds\": %.3f, "
-           "\"us_per_call\": %.3f, \"all_walks_seconds\": %.1f}, \"chars\": %zu}\n",
+           "\"us_per_call\": %.3f, \"all_walks_seconds\": %.1f}, \"affected_walks_of_small_batches\": %s, \"chars\": %zu}\n",
            (unsigned long long)W, (unsigned long long)n_old, t_old, 1e6 * t_old / n_old, t_old / n_old * W,
-           (unsigned long long)n_new, t_new, 1e6 * t_new / n_new, t_new / n_new * W, total);
+           (unsigned long long)n_new, t_new, 1e6 * t_new / n_new, t_new / n_new * W, sparse.c_str(), total);
     wharf_destroy(h);
     return 0;
 }
