@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Refresh the committed rocprofv3 records from one profiling session
-(`tools/gpu_round3.sh prof pmc`): copies the kernel statistics, a filtered
+(`OUTDIR=gpurun_out/r4 tools/gpu_session.sh prof pmc`): copies the kernel statistics, a filtered
 kernel trace and the PMC passes into profiles/<round>/rocprof/, and writes the
 per-launch HBM summaries bench.py reads (profiles/pmc_<round>_*.json).
 
@@ -9,7 +9,7 @@ request, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both KiB, from separate passes
 Durations come from the kernel trace of the default bench run under the
 profiler (timed launches only for generation: dispatch order 3-7).
 
-    python tools/pmc_session.py gpurun_out/r3 r03
+    python tools/pmc_session.py gpurun_out/r4 r04
 """
 import csv
 import json
