@@ -5,7 +5,7 @@
 // the host snapshot, on configs[1]'s graph (RMAT scale 22, 117 M samples, wpv 10, L 80).
 // Then the reference's incremental pattern (vertex-classification.cpp:171-176):
 // after each insert batch of the throughput driver's sizes (5 / 50 / 500
-// directed edges, throughput-latency.cpp:87-93,121), walk(i) of the affected
+// directed edges between low-degree vertices, throughput-latency.cpp:87-93), walk(i) of the affected
 // walks only — with the snapshot chunk taken once 32 of its walks were read
 // (default), taken on the first read (WHARF_WALK_FILL_AFTER=0, round 3), and a
 // device read per call.
@@ -46,6 +46,8 @@ int main(int argc, char** argv)
         total += len;
     }
     const double t_old = now() - t0;
+    printf("per-call device reads: %llu walks in %.3f s\n", (unsigned long long)n_old, t_old);
+    fflush(stdout);
     unsetenv("WHARF_WALK_NO_SNAPSHOT");
     t0 = now();
     for (uint64_t i = 0; i < n_new; i++) {
@@ -53,15 +55,24 @@ int main(int argc, char** argv)
         total += len;
     }
     const double t_new = now() - t0;
+    printf("host snapshot: %llu walks in %.3f s\n", (unsigned long long)n_new, t_new);
+    fflush(stdout);
     // sparse: the affected walks of small batches
     std::vector<uint32_t> aff(W), pairs;
     std::string sparse = "[";
     for (uint64_t bs : {5ull, 50ull, 500ull}) {
+        // edges between low-degree vertices (RMAT's upper id half), so the affected walks are a
+        // sparse set: an RMAT batch of any size touches hubs that most walks visit
         pairs.assign(2 * bs, 0);
-        uint64_t cnt = 0, naff = 0;
-        if (wharf_generate_batch_of_edges(0, bs, n, 1000 + bs, 0, 1, 0.5, 0.2, 0.1, pairs.data(), &cnt) ||
-            wharf_insert_edges(h, cnt, pairs.data(), WHARF_REMOVE_DUPS | WHARF_APPLY_WALK_UPDATES, aff.data(), &naff))
+        uint64_t cnt = bs, naff = 0, x = 88172645463325252ull + bs;
+        for (uint64_t i = 0; i < 2 * bs; i++) {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            pairs[i] = (uint32_t)(n / 2 + x % (n / 2));
+        }
+        if (wharf_insert_edges(h, cnt, pairs.data(), WHARF_REMOVE_DUPS | WHARF_APPLY_WALK_UPDATES, aff.data(), &naff))
             return 4;
+        printf("batch of %llu edges: %llu affected walks\n", (unsigned long long)cnt, (unsigned long long)naff);
+        fflush(stdout);
         const char* modes[3][2] = {{"fill_after_32", nullptr}, {"fill_on_first_read", "0"}, {"device_read_per_call", nullptr}};
         std::string rec = "{\"batch_edges\": " + std::to_string(cnt) + ", \"affected\": " + std::to_string(naff);
         for (int m = 0; m < 3; m++) {
@@ -82,6 +93,8 @@ int main(int argc, char** argv)
             char part[160];
             snprintf(part, sizeof part, ", \"%s_ms\": %.3f", modes[m][0], 1e3 * t);
             rec += part;
+            printf("  %s: %.3f ms\n", modes[m][0], 1e3 * t);
+            fflush(stdout);
         }
         sparse += (sparse.size() > 1 ? ", " : "") + rec + "}";
         unsetenv("WHARF_WALK_FILL_AFTER");
