@@ -10,6 +10,7 @@
 #                             BASELINE's 8-GPU jobs (configs[3], configs[4]) at scale - 4
 #   bigscale:<args>           tools/bigscale.py with args (',' for spaces)
 #   probe:<args>              tools/rewalk_probe.py with args (',' for spaces)
+#   py:<script args>          python -u <script args> (',' for spaces)
 #   exe:<cmd>                 a built probe, e.g. exe:tools/sort_probe (',' for spaces)
 #   rocprof:<script args>     rocprofv3 --kernel-trace --stats of python3 <script args> (',' for spaces)
 #   ab:<names>                ${AB_SCRIPT:-tools/rewalk_probe.py} $PROBE_ARGS with tools/ab/lib_<name>.so per
@@ -57,6 +58,9 @@ for step in "$@"; do
     probe)
         timeout -k 10 900 python -u tools/rewalk_probe.py $args > "$log" 2>&1
         rc=$?; tail -4 "$log" ;;
+    py)   # py:<script and args>: any python tool of the tree, output streamed to its log
+        timeout -k 10 900 python -u $args > "$log" 2>&1
+        rc=$?; tail -3 "$log" ;;
     exe)
         timeout -k 10 300 $args > "$log" 2>&1
         rc=$?; tail -3 "$log" ;;
