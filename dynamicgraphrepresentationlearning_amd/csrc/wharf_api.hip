@@ -140,6 +140,15 @@ struct wharf_handle {
     size_t snap_next = 0, snap_cap = 0;
     std::vector<uint32_t> one_row;    // the last walk read on its own (vertex_at_walk(i, p) for p = 0, 1, ...)
     uint64_t one_li = ~0ull, one_version = ~0ull;
+    // The affected walks of the last update (the reference's incremental readout calls walk(i) for
+    // exactly those, vertex-classification.cpp:171-176): when the update handed its ids to the host
+    // and there are at most kStageMax, the first walk() of one of them stages all their rows with one
+    // list gather and one copy.
+    static constexpr uint64_t kStageMax = 1ull << 20;
+    std::vector<uint32_t> last_aff;   // ascending global ids of the last update's affected walks
+    uint64_t last_aff_version = ~0ull, stage_version = ~0ull;
+    std::vector<uint64_t> stage_li;   // their local indices (ascending), and their rows
+    std::vector<uint32_t> stage_rows;
 
     void walks_changed() { walks_version++; }
 
@@ -173,6 +182,7 @@ struct wharf_handle {
         }
         if (snap_of[c] >= 0) return snaps[snap_of[c]].host + (li - c * kSnapWalks) * L;
         if (one_version == walks_version && one_li == li) return one_row.data();
+        if (const uint32_t* r = staged_row(li)) return r;
         const char* fa = getenv("WHARF_WALK_FILL_AFTER");   // A/B (tools/walk_readout): 0 = round 3's rule
         const uint32_t fill_after = fa && *fa ? (uint32_t)atoi(fa) : kSnapFillAfter;
         if (snap_reads[c] < fill_after) {   // sparse so far: this row alone
@@ -207,6 +217,33 @@ struct wharf_handle {
         snap_of[c] = (int64_t)slot;
         return snaps[slot].host + (li - base) * L;
     }
+    // the row of li from the affected-walk stage of the last update, or null
+    const uint32_t* staged_row(uint64_t li)
+    {
+        if (last_aff_version != walks_version || last_aff.empty()) return nullptr;
+        if (stage_version != walks_version) {
+            // stage only when li is one of them (a reader of other walks never pays for it)
+            const uint64_t r = li / n_loc, wid = r * n + lo + (li - r * n_loc);
+            if (!std::binary_search(last_aff.begin(), last_aff.end(), (uint32_t)wid)) return nullptr;
+            const uint64_t k = last_aff.size();
+            stage_li.resize(k);
+            for (uint64_t i = 0; i < k; i++) {
+                const uint64_t w = last_aff[i], rr = w / n;
+                stage_li[i] = rr * n_loc + (w % n - lo);
+            }
+            count.ensure(k * 8);
+            HIPCHK(hipMemcpyAsync(count.p, stage_li.data(), k * 8, hipMemcpyHostToDevice, s));
+            sel.ensure(k * L * 4);
+            launch_gather_rows(walks.as<uint32_t>(), W, L, count.as<uint64_t>(), 0, k, sel.as<uint32_t>(), s);
+            stage_rows.resize(k * L);
+            HIPCHK(hipMemcpyAsync(stage_rows.data(), sel.p, k * L * 4, hipMemcpyDeviceToHost, s));
+            sync();
+            stage_version = walks_version;
+        }
+        const auto it = std::lower_bound(stage_li.begin(), stage_li.end(), li);
+        if (it == stage_li.end() || *it != li) return nullptr;
+        return stage_rows.data() + (uint64_t)(it - stage_li.begin()) * L;
+    }
     void free_snaps()
     {
         for (Snap& x : snaps)
@@ -216,6 +253,10 @@ struct wharf_handle {
         snap_reads.clear();
         snap_next = 0;
         one_li = ~0ull;
+        last_aff.clear();
+        stage_li.clear();
+        stage_rows.clear();
+        last_aff_version = stage_version = ~0ull;
     }
 
     void sync() { HIPCHK(hipStreamSynchronize(s)); }
@@ -966,6 +1007,19 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         if (affected_out && !on_device && naff) {
             HIPCHK(hipMemcpyAsync(affected_out, h->pairs.p, naff * 4, hipMemcpyDeviceToHost, s));
             h->sync();
+        }
+        // the ids for walk()'s affected-walk stage (host callers, at most kStageMax of them)
+        h->last_aff.clear();
+        h->last_aff_version = ~0ull;
+        if (!on_device && naff && naff <= wharf_handle::kStageMax) {
+            if (affected_out) {
+                h->last_aff.assign(affected_out, affected_out + naff);
+            } else {
+                h->last_aff.resize(naff);
+                HIPCHK(hipMemcpyAsync(h->last_aff.data(), h->pairs.p, naff * 4, hipMemcpyDeviceToHost, s));
+                h->sync();
+            }
+            h->last_aff_version = h->walks_version;
         }
         h->st.affected = naff;
         if (n_affected) *n_affected = naff;

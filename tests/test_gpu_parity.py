@@ -619,7 +619,8 @@ def test_walk_rows_export_and_sparse_readout(W):
     chunked corpus gather's source) equals the whole export on any row range;
     walk() of a few walks per 64 Ki-walk chunk reads them one by one (ADVICE r3:
     no chunk pulled for a sparse affected-walk readout), a dense readout takes the
-    chunk, and both agree with the export after every change."""
+    chunk, the affected walks of an update are staged together on the first read
+    of one of them, and all agree with the export after every change."""
     import torch
     base = O.generate_batch_of_edges(60000, 1 << 18, 4, False, False)
     off, adj = O.csr_from_edges(1 << 17, base)
@@ -645,8 +646,19 @@ def test_walk_rows_export_and_sparse_readout(W):
         for i in range(1 << 16, 1 << 17):
             assert g.walk_vertices(i).tolist() == full[i][full[i] != W.SENTINEL].tolist()
         b = O.generate_batch_of_edges(2000, 1 << 17, 20 + rnd, False, False)
-        g.insert_edges_batch(b, remove_dups=True)
+        aff = g.insert_edges_batch(b, remove_dups=True)
         full = g.walks()
+        # the reference's incremental readout: walk(i) of the affected walks (staged together)
+        for i in aff[::max(1, len(aff) // 3000)]:
+            assert g.walk(int(i)) == O.walk_string(full[i])
+    # an update whose walks are staged, then a read of an unaffected walk, then of affected ones
+    b = O.generate_batch_of_edges(30, 1 << 17, 77, False, False)
+    aff = g.insert_edges_batch(b, remove_dups=True)
+    full = g.walks()
+    other = int(np.setdiff1d(np.arange(Wn), aff)[5])
+    assert g.walk(other) == O.walk_string(full[other])
+    for i in aff:
+        assert g.walk_vertices(int(i)).tolist() == full[i][full[i] != W.SENTINEL].tolist()
     g.destroy()
 
 
