@@ -95,6 +95,9 @@ def parse():
     p.add_argument("--job-gather", type=int, default=1, help="time the jobs' bounded corpus all-gatherv (0 = off)")
     p.add_argument("--job-one-gpu", type=int, default=1,
                    help="configs[3] job: rank 0 also runs every walk on its GPU (the 1-GPU time) (0 = off)")
+    p.add_argument("--job-shards", choices=["blocks", "ranges"], default="blocks",
+                   help="jobs' walk shards: vertex blocks dealt round-robin (balanced mix) or contiguous ranges")
+    p.add_argument("--job-block-bits", type=int, default=16, help="block size (log2 vertices) of --job-shards blocks")
     p.add_argument("--gather-chunk-bytes", type=int, default=4 << 30,
                    help="device buffer of the bounded corpus gather (all ranks' rows of one chunk)")
     p.add_argument("--gather-check", type=int, default=1,
@@ -594,8 +597,7 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
     pass (the chunk is dropped), then a checked pass: the checksum of everything
     every rank received equals the sum of the ranks' local checksums."""
     from dynamicgraphrepresentationlearning_amd.distributed import corpus_checksum, gather_corpus_chunked, \
-        local_corpus_checksum
-    lo, hi = shards[rank]
+        local_corpus_checksum, shard_size
     on_dev = comm_dev != "cpu"
     K = max(1, int(budget_bytes // (world * L * 4)))
     stage = None if on_dev else torch.empty((K, L), dtype=torch.int32, device=f"cuda:{dev}")
@@ -615,7 +617,8 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
     ms_all = _max_over_ranks(torch, dist, comm_dev, [ms])[0]
     rec = {"pattern": "gather_corpus_chunked: full-mesh batch_isend_irecv per chunk of local rows",
            "backend": "nccl (RCCL over xGMI)" if on_dev else "gloo (host staging)",
-           "walks": sum(h_ - l_ for l_, h_ in shards) * wpv, "corpus_bytes": sum(h_ - l_ for l_, h_ in shards) * wpv * L * 4,
+           "walks": sum(shard_size(sh) for sh in shards) * wpv,
+           "corpus_bytes": sum(shard_size(sh) for sh in shards) * wpv * L * 4,
            "rows_per_rank_per_chunk": K,
            "buffer_bytes": K * world * L * 4, "chunks": st["chunks"], "ms": round(ms_all, 2),
            "bytes_received_rank0": int(st["bytes_received"]),
@@ -628,7 +631,7 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
                 acc.add_(corpus_checksum(chunk[r0:r0 + c], g0, L))
 
         gather_corpus_chunked(read_local, shards, n, wpv, L, K, sink, device=comm_dev)
-        mine = local_corpus_checksum(read_local, lo, hi, n, wpv, L, K, device=comm_dev)
+        mine = local_corpus_checksum(read_local, shards[rank], n, wpv, L, K, device=comm_dev)
         tot = mine.clone()
         if dist:
             dist.all_reduce(tot)
@@ -664,7 +667,7 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
     throughput-latency.cpp:126,135).  Per update: barrier, the rank's wall time,
     max over ranks.  configs[3] also runs, on rank 0 alone, every walk on one
     GPU over the same graph: the 1-GPU time the job divides."""
-    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards
+    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards, block_shards, shard_size
     spec = JOBS[name]
     scale = spec["scale"] + args.job_scale_delta
     samples = spec["samples"] >> (-args.job_scale_delta) if args.job_scale_delta < 0 else spec["samples"]
@@ -677,10 +680,11 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
     try:
         t0 = time.time()
         g = W.WharfMH.from_rmat(n, samples, 2 * n, seed=4, config=cfg, device=dev)
-        deg = np.diff(g.offsets().astype(np.int64))
-        shards = balanced_shards(deg, parts)
-        lo, hi = shards[rank]
-        g.set_shard(lo, hi)
+        if args.job_shards == "blocks":   # 64 Ki-vertex blocks round-robin: every rank the same mix
+            shards = block_shards(n, parts, args.job_block_bits)
+        else:                               # contiguous ranges with equal non-isolated vertex counts
+            shards = balanced_shards(np.diff(g.offsets().astype(np.int64)), parts)
+        g.apply_shard(shards[rank])
         build_s = time.time() - t0
         gen = []
         for _ in range(2):   # first (node2vec: every anchor initialised) and warm generation
@@ -696,7 +700,9 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
         rec = {"workload": f"BASELINE {name}: {spec['desc']}; RMAT scale {scale}, {samples} undirected samples "
                            f"(seed 4), m={g.number_of_edges()}",
                "ranks": world, "walk_shards": parts,
-               "walks_this_run": int(sum(hi_ - lo_ for lo_, hi_ in shards[:world]) * 10),
+               "shard_kind": f"blocks of 2^{args.job_block_bits} vertices round-robin"
+               if args.job_shards == "blocks" else "contiguous ranges, equal non-isolated counts",
+               "walks_this_run": int(sum(shard_size(sh) for sh in shards[:world]) * 10),
                "walks_whole_job": n * 10, "scaling": "strong (the job's walks split over the ranks)"
                if spec["split"] == "ranks" else f"weak (rank g runs shard g of {parts}: {world}/{parts} of the job)",
                "build_s_rank0": round(build_s, 1),

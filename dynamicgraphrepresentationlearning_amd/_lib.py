@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # WHARF_LIB_PATH: an alternative build of the same library (A/B experiments in tools/)
 LIB_PATH = os.environ.get("WHARF_LIB_PATH") or os.path.join(_HERE, "libwharf_gpu.so")
 
-ABI_VERSION = 5   # WHARF_ABI_VERSION of include/wharf_gpu.h
+ABI_VERSION = 6   # WHARF_ABI_VERSION of include/wharf_gpu.h
 WHARF_OK = 0
 WHARF_DEEPWALK, WHARF_NODE2VEC = 0, 1
 WHARF_INIT_RANDOM, WHARF_INIT_BURNIN, WHARF_INIT_WEIGHT = 0, 1, 2
@@ -97,6 +97,8 @@ SIGNATURES = {
     "wharf_number_of_edges": (_I, [_P, _P]),
     "wharf_shard": (_I, [_P, _P, _P, _P]),
     "wharf_set_shard": (_I, [_P, _U64, _U64]),
+    "wharf_set_shard_blocks": (_I, [_P, _U32, _U32, _U32]),
+    "wharf_shard_blocks": (_I, [_P, _P, _P, _P]),
     "wharf_get_graph": (_I, [_P, _P, _P]),
     "wharf_walk": (_I, [_P, _U64, _P, _P]),
     "wharf_walk_string": (_I, [_P, _U64, _P, C.c_size_t, _P]),

@@ -64,6 +64,13 @@ struct DevBuf {
         HIPCHK(hipMalloc(&p, b));
         cap = b;
     }
+    // per-batch buffers: 1/4 headroom, so batches of varying size do not free and
+    // re-allocate them every time (a hipMalloc costs the update ~0.1 ms)
+    void ensure_grow(size_t bytes)
+    {
+        if (bytes <= cap && p) return;
+        ensure(bytes + bytes / 4);
+    }
     void release()
     {
         if (p) (void)hipFree(p);
@@ -88,6 +95,19 @@ struct wharf_handle {
     hipEvent_t ev[6] = {};
     wharf_config cfg{};
     uint64_t n = 0, m = 0, lo = 0, hi = 0, n_loc = 0, W = 0;
+    uint32_t sh_part = 0, sh_parts = 1, sh_bits = 0;   // block shard (wharf_set_shard_blocks); contiguous: 0, 1, 0
+
+    ShardMap smap() const { return ShardMap{n, n_loc, lo, sh_part, sh_parts, sh_bits}; }
+    // the local column of walk wid, if this handle owns it
+    bool owned_li(uint64_t wid, uint64_t& li) const
+    {
+        const uint64_t r = wid / n, v = wid % n;
+        if (r >= wpv || v < lo || v >= hi) return false;
+        const uint64_t off = v - lo, q = off >> sh_bits;
+        if (q % sh_parts != sh_part) return false;
+        li = r * n_loc + (((q / sh_parts) << sh_bits) | (off & ((1ull << sh_bits) - 1)));
+        return true;
+    }
     uint32_t L = 0, wpv = 0;
     bool anchors = false, has_walks = false;
     bool anchors_cold = true;                  // node2vec MH: no generation has filled the anchor cache yet
@@ -223,14 +243,12 @@ struct wharf_handle {
         if (last_aff_version != walks_version || last_aff.empty()) return nullptr;
         if (stage_version != walks_version) {
             // stage only when li is one of them (a reader of other walks never pays for it)
-            const uint64_t r = li / n_loc, wid = r * n + lo + (li - r * n_loc);
+            const uint64_t wid = smap().wid(li);
             if (!std::binary_search(last_aff.begin(), last_aff.end(), (uint32_t)wid)) return nullptr;
             const uint64_t k = last_aff.size();
             stage_li.resize(k);
-            for (uint64_t i = 0; i < k; i++) {
-                const uint64_t w = last_aff[i], rr = w / n;
-                stage_li[i] = rr * n_loc + (w % n - lo);
-            }
+            for (uint64_t i = 0; i < k; i++)
+                if (!owned_li(last_aff[i], stage_li[i])) throw WharfError(WHARF_E_STATE, "affected walk not owned");
             count.ensure(k * 8);
             HIPCHK(hipMemcpyAsync(count.p, stage_li.data(), k * 8, hipMemcpyHostToDevice, s));
             sel.ensure(k * L * 4);
@@ -588,7 +606,7 @@ struct wharf_handle {
     void update_filters(const RunInfo* runs_d, uint64_t k)
     {
         if (!fpool.p || !k) return;
-        fplan.ensure((k + 1) * 16);
+        fplan.ensure_grow((k + 1) * 16);
         uint64_t* need = fplan.as<uint64_t>();
         uint64_t* gofs = need + k + 1;
         launch_filter_plan(runs_d, k, deg.as<uint32_t>(), fdir.as<uint64_t>(), need, s);
@@ -627,6 +645,7 @@ struct wharf_handle {
         a.aff = aff.as<uint8_t>();
         a.counters = counters.as<unsigned long long>();
         a.n = n; a.n_loc = n_loc; a.lo = lo; a.W = W; a.wpv = wpv;
+        a.sh_part = sh_part; a.sh_parts = sh_parts; a.sh_bits = sh_bits;
         a.L = L; a.epoch = epoch;
         a.key0 = (uint32_t)cfg.seed; a.key1 = (uint32_t)(cfg.seed >> 32);
         a.inv_p = 1.0f / cfg.paramP;   // node2vec.h:81 `1 / this->paramP` in float
@@ -924,7 +943,7 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         const bool preinit = no_pre && *no_pre ? atoi(no_pre) == 0 : dense;
         if (a.model == kNode2Vec && !a.det && a.anchor && !a.scan_only && k && preinit) {
             // the batch's invalidated anchors, computed ahead of the re-walk (k_anchor_preinit)
-            h->preoff.ensure((k + 1) * 16);
+            h->preoff.ensure_grow((k + 1) * 16);
             uint64_t* degs = h->preoff.as<uint64_t>();
             uint64_t* preoff = degs + (k + 1);
             launch_source_degrees(h->runs.as<RunInfo>(), k, h->vrec.as<ERec>(), degs, s);
@@ -993,7 +1012,7 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         });
         const bool on_device = affected_out && (flags & WHARF_AFFECTED_DEVICE);
         if (!on_device) h->pairs.ensure(h->W * 4);
-        launch_aff_write(h->aff.as<uint8_t>(), h->W, boff, h->n, h->n_loc, h->lo,
+        launch_aff_write(h->aff.as<uint8_t>(), h->W, boff, h->smap(),
                          on_device ? affected_out : h->pairs.as<uint32_t>(), s);
         uint32_t naff32 = 0;
         unsigned long long lerr = 0;
@@ -1050,9 +1069,9 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         hipStream_t s = h->s;
         // 1. batch -> device keys, validated, sorted by (src, dst), deduplicated
         //    (wharfmh.h:450-470, 1056-1104)
-        h->pairs.ensure(m * 8);
-        h->k1.ensure(m * 8);
-        h->k2.ensure(m * 8);
+        h->pairs.ensure_grow(m * 8);
+        h->k1.ensure_grow(m * 8);
+        h->k2.ensure_grow(m * 8);
         HIPCHK(hipMemcpyAsync(h->pairs.p, pairs, m * 8, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemsetAsync(h->errflag.p, 0, 8, s));
         launch_pairs_to_keys(h->pairs.as<uint32_t>(), m, h->n, h->k1.as<uint64_t>(),
@@ -1067,9 +1086,9 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         uint64_t* bkeys = h->k1.as<uint64_t>();
 
         // 2. source runs (pack_index, wharfmh.h:475-481)
-        h->flags.ensure(mb);
+        h->flags.ensure_grow(mb);
         launch_run_flags(bkeys, mb, h->flags.as<uint8_t>(), s);
-        h->runstart.ensure(mb * 4);
+        h->runstart.ensure_grow(mb * 4);
         {
             auto cnt_it = rocprim::counting_iterator<uint32_t>(0);
             uint8_t* fl = h->flags.as<uint8_t>();
@@ -1078,8 +1097,8 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             h->rp([&](void* t, size_t& b) { return rocprim::select(t, b, cnt_it, fl, rsp, c, (size_t)mb, s); });
         }
         // 3. which batch edges change their row (uniont / difference), exclusive scan
-        h->chg.ensure((mb + 1) * 4);
-        h->cf.ensure((mb + 1) * 4);
+        h->chg.ensure_grow((mb + 1) * 4);
+        h->cf.ensure_grow((mb + 1) * 4);
         HIPCHK(hipMemsetAsync(h->chg.as<uint32_t>() + mb, 0, 4, s));
         launch_batch_change(bkeys, mb, h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->adj.as<uint32_t>(), insert,
                             h->chg.as<uint32_t>(), s);
@@ -1112,9 +1131,9 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         // the batch can no longer fail: after the pool planning below.
         REQUIRE(h->epoch + 1 < (1u << kEpochBits), WHARF_E_INVALID, "update epoch limit (2^24 applied batches) reached");
         const uint32_t epoch = h->epoch + 1;
-        h->runs.ensure(k * sizeof(RunInfo));
-        h->rplan.ensure(k * sizeof(RowPlan));
-        h->pscan.ensure((k + 1) * 32);
+        h->runs.ensure_grow(k * sizeof(RunInfo));
+        h->rplan.ensure_grow(k * sizeof(RowPlan));
+        h->pscan.ensure_grow((k + 1) * 32);
         uint64_t* need = h->pscan.as<uint64_t>();
         uint64_t* save = need + (k + 1);
         uint64_t* relofs = save + (k + 1);
@@ -1159,13 +1178,13 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         const char* acv = getenv("WHARF_ANCHOR_CARRY");
         const bool carry = h->anchors && h->symmetric && !(acv && *acv && atoi(acv) == 0);
         uint64_t* anc_base = h->anchors ? h->erec.as<uint64_t>() + 2 : nullptr;
-        if (carry) h->sanc.ensure(std::max<uint64_t>(saved, 1) * 8);
+        if (carry) h->sanc.ensure_grow(std::max<uint64_t>(saved, 1) * 8);
         h->grown = grow;
-        h->scratch.ensure(std::max<uint64_t>(saved, 1) * 4);
+        h->scratch.ensure_grow(std::max<uint64_t>(saved, 1) * 4);
         h->start_bound = saved + (insert ? total_chg : 0);   // the sources' degrees after the update, at most
         const uint32_t rs = (uint32_t)h->rec_stride();
         // source rows in chunks: counts of each run's longest range, exclusive prefix (k_run_chunks)
-        h->rchunk.ensure((k + 1) * 8);
+        h->rchunk.ensure_grow((k + 1) * 8);
         uint32_t* rcnt = h->rchunk.as<uint32_t>();
         uint32_t* rpre = rcnt + (k + 1);
         launch_run_chunks(h->runs.as<RunInfo>(), h->rplan.as<RowPlan>(), k, rcnt, s);
@@ -1467,11 +1486,55 @@ int wharf_set_shard(wharf_handle* h, uint64_t lo, uint64_t hi)
         h->lo = lo;
         h->hi = hi;
         h->n_loc = hi - lo;
+        h->sh_part = 0;
+        h->sh_parts = 1;
+        h->sh_bits = 0;
         h->W = h->n_loc * h->wpv;
         h->cfg.shard_lo = lo;
         h->cfg.shard_hi = hi;
         h->has_walks = false;
     });
+}
+
+int wharf_set_shard_blocks(wharf_handle* h, uint32_t part, uint32_t parts, uint32_t block_bits)
+{
+    return guarded(h, [&] {
+        REQUIRE(h, WHARF_E_INVALID, "null handle");
+        REQUIRE(parts >= 1 && part < parts, WHARF_E_INVALID, "block shard: need part < parts");
+        REQUIRE(block_bits >= 6 && block_bits < 32, WHARF_E_INVALID, "block shard: block_bits must be 6..31");
+        REQUIRE((h->n * h->wpv) < (1ull << 32), WHARF_E_INVALID, "n * walks_per_vertex must be < 2^32");
+        // owned vertices: the part's blocks of 2^bits, round-robin; only the graph's last block can be short
+        const uint64_t B = 1ull << block_bits, nblocks = (h->n + B - 1) / B;
+        uint64_t n_loc = 0;
+        for (uint64_t q = part; q < nblocks; q += parts) n_loc += std::min(B, h->n - q * B);
+        h->sync();
+        h->walks.release();
+        h->walks_changed();
+        h->free_snaps();
+        h->aff.release();
+        h->defer.release();
+        h->park.release();
+        h->bdesc.release();
+        h->lo = 0;
+        h->hi = h->n;
+        h->n_loc = n_loc;
+        h->sh_part = part;
+        h->sh_parts = parts;
+        h->sh_bits = block_bits;
+        h->W = n_loc * h->wpv;
+        h->cfg.shard_lo = 0;
+        h->cfg.shard_hi = 0;
+        h->has_walks = false;
+    });
+}
+
+int wharf_shard_blocks(const wharf_handle* h, uint32_t* part, uint32_t* parts, uint32_t* block_bits)
+{
+    if (!h) return WHARF_E_INVALID;
+    if (part) *part = h->sh_part;
+    if (parts) *parts = h->sh_parts;
+    if (block_bits) *block_bits = h->sh_bits;
+    return WHARF_OK;
 }
 
 int wharf_get_graph(wharf_handle* h, uint64_t* offsets_out, uint32_t* targets_out)
@@ -1503,10 +1566,9 @@ static bool no_snapshot()
 
 static uint64_t local_index(wharf_handle* h, uint64_t wid)
 {
-    const uint64_t r = wid / h->n, v = wid % h->n;
-    REQUIRE(r < h->wpv && v >= h->lo && v < h->hi, WHARF_E_RANGE,
-            "walk " + std::to_string(wid) + " is not owned by this handle");
-    return r * h->n_loc + (v - h->lo);
+    uint64_t li = 0;
+    REQUIRE(h->owned_li(wid, li), WHARF_E_RANGE, "walk " + std::to_string(wid) + " is not owned by this handle");
+    return li;
 }
 
 int wharf_walk(wharf_handle* h, uint64_t wid, uint32_t* out, uint32_t* len)
@@ -1677,8 +1739,7 @@ int wharf_walk_ids(wharf_handle* h, uint32_t* ids)
     return guarded(h, [&] {
         REQUIRE(h && ids, WHARF_E_INVALID, "null argument");
         for (uint64_t li = 0; li < h->W; li++) {
-            const uint64_t r = li / h->n_loc;
-            ids[li] = (uint32_t)(r * h->n + h->lo + (li - r * h->n_loc));
+            ids[li] = (uint32_t)h->smap().wid(li);
         }
     });
 }
@@ -1711,7 +1772,7 @@ uint64_t build_index(wharf_handle* h, int& kb, uint64_t v0, uint64_t v1)
     h->k2.ensure(E * 8);
     h->flags.ensure(E * 4);
     h->pairs.ensure(E * 4);
-    launch_index_entries(h->walks.as<uint32_t>(), W, h->L, h->n, h->n_loc, h->lo, kb, (uint32_t)v0, (uint32_t)v1, base,
+    launch_index_entries(h->walks.as<uint32_t>(), W, h->L, h->smap(), kb, (uint32_t)v0, (uint32_t)v1, base,
                          h->k1.as<uint64_t>(), h->flags.as<uint32_t>(), h->s);
     uint64_t* ki = h->k1.as<uint64_t>();
     uint64_t* ko = h->k2.as<uint64_t>();

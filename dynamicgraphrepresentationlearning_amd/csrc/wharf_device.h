@@ -99,6 +99,27 @@ __host__ __device__ __forceinline__ uint32_t filt_log2_words(uint64_t deg)
     return lg;
 }
 
+// Which walks a handle owns.  Walk id wid = r * n + v (round r,
+// start vertex v, wharfmh.h:275-292); the handle's local column li = r * n_loc + j,
+// where the j-th owned start vertex is
+//   contiguous shard [lo, hi):  v = lo + j                       (parts = 1)
+//   block shard (part of parts): the part's blocks of 2^bits vertices, dealt
+//     round-robin: v = ((j >> bits) * parts + part) << bits | (j & (2^bits - 1))
+// Both are increasing in j, so ascending columns are ascending walk ids.
+struct ShardMap {
+    uint64_t n, n_loc, lo;
+    uint32_t part, parts, bits;
+    __host__ __device__ __forceinline__ uint64_t vertex(uint64_t j) const
+    {
+        return lo + ((((j >> bits) * parts + part) << bits) | (j & ((1ull << bits) - 1)));
+    }
+    __host__ __device__ __forceinline__ uint64_t wid(uint64_t li) const
+    {
+        const uint64_t r = li / n_loc;
+        return r * n + vertex(li - r * n_loc);
+    }
+};
+
 __host__ __device__ __forceinline__ ERec make_rec(uint32_t v, uint32_t deg, uint64_t off, uint32_t epoch)
 {
     ERec r;

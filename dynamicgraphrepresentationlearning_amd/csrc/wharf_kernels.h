@@ -37,6 +37,7 @@ struct WalkArgs {
     uint8_t* aff;                // per owned walk: re-walk position or kNoRewalk
     unsigned long long* counters;  // [0] steps, [1] accepts, [2] re-walk list, [3..6] WHARF_INIT_STATS, [7] anchor inits
     uint64_t n, n_loc, lo, W;
+    uint32_t sh_part, sh_parts, sh_bits;   // the shard's blocks (ShardMap; contiguous: 0, 1, 0)
     uint32_t L, epoch;
     uint32_t key0, key1;
     float inv_p, inv_q;
@@ -63,6 +64,11 @@ struct WalkArgs {
     unsigned long long* err;     // re-walk list consumers: bit 0 an entry out of range, bit 1 an entry outside its block
     int stage;                   // node2vec re-walk launch: 0 plan + consumer, 1 plan only, 2 consumer only
 };
+
+__host__ __device__ __forceinline__ ShardMap shard_map(const WalkArgs& a)
+{
+    return ShardMap{a.n, a.n_loc, a.lo, a.sh_part, a.sh_parts, a.sh_bits};
+}
 
 constexpr uint64_t kListMask = (1ull << 40) - 1;   // counters[2]: tickets << 40 | re-walk list entries
 constexpr uint64_t kParkRecBytes = 32;   // one parked walker of the node2vec re-walk passes
@@ -148,14 +154,14 @@ void launch_gather_rows(const uint32_t* walks, uint64_t W, uint32_t L, const uin
                         uint64_t count, uint32_t* out, hipStream_t s);
 void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint32_t v0, uint32_t v1, uint64_t* len,
                          hipStream_t s);
-void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc, uint64_t lo, int kb,
+void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, const ShardMap& sm, int kb,
                           uint32_t v0, uint32_t v1, const uint64_t* col_base, uint64_t* skeys, uint32_t* vals,
                           hipStream_t s);
 void launch_index_split(const uint64_t* skeys, uint64_t E, int kb, unsigned long long* counts, uint64_t* keys,
                         hipStream_t s);
 unsigned aff_blocks(uint64_t W);
 void launch_aff_count(const uint8_t* aff, uint64_t W, uint32_t* counts, hipStream_t s);
-void launch_aff_write(const uint8_t* aff, uint64_t W, const uint32_t* offs, uint64_t n, uint64_t n_loc, uint64_t lo,
+void launch_aff_write(const uint8_t* aff, uint64_t W, const uint32_t* offs, const ShardMap& sm,
                       uint32_t* out, hipStream_t s);
 void launch_index_pair(const uint64_t* keys, const uint32_t* nexts, uint64_t E, uint64_t* out, hipStream_t s);
 void launch_rel_offsets(const uint64_t* off, uint64_t v0, uint64_t cnt, uint32_t* rel, hipStream_t s);

@@ -705,7 +705,7 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
     const uint64_t W = a.W;
     for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += stride) {
         const uint64_t r = li / a.n_loc;
-        const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
+        const uint32_t v = (uint32_t)shard_map(a).vertex(li - r * a.n_loc);
         const uint64_t wid = r * a.n + v;
         const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
         const uint64_t* __restrict__ rt = DET ? a.rtab + r * a.L : nullptr;
@@ -769,7 +769,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
     const uint32_t L = a.L;
     for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += stride) {
         const uint64_t r = li / a.n_loc;
-        const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
+        const uint32_t v = (uint32_t)shard_map(a).vertex(li - r * a.n_loc);
         const uint64_t wid = r * a.n + v;
         const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
         const uint64_t* __restrict__ rt = DET ? a.rtab + r * L : nullptr;
@@ -1603,7 +1603,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
             li = ent & ((1ull << 56) - 1);
             p = (uint32_t)(ent >> 56);
             const uint64_t r = li / a.n_loc;
-            const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
+            const uint64_t wid = r * a.n + shard_map(a).vertex(li - r * a.n_loc);
             wlo = (uint32_t)wid;
             whi = (uint32_t)(wid >> 32);
             if constexpr (DET) rt = a.rtab + r * L;
@@ -1680,7 +1680,7 @@ __global__ __launch_bounds__(256) void k_rewalk_block(WalkArgs a)
             li = ent & ((1ull << 56) - 1);
             p = (uint32_t)(ent >> 56);
             const uint64_t r = li / a.n_loc;
-            const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
+            const uint64_t wid = r * a.n + shard_map(a).vertex(li - r * a.n_loc);
             wlo = (uint32_t)wid;
             whi = (uint32_t)(wid >> 32);
             pcol[li - base] = p;
@@ -1750,7 +1750,7 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
             p = (uint32_t)(e >> 56);
             if (!list_entry_ok(a, li, p)) continue;
             const uint64_t r = li / a.n_loc;
-            const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
+            const uint64_t wid = r * a.n + shard_map(a).vertex(li - r * a.n_loc);
             wlo = (uint32_t)wid;
             whi = (uint32_t)(wid >> 32);
             if constexpr (DET) rt = a.rtab + r * L;
@@ -1829,7 +1829,7 @@ __global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* 
                 }
                 pos = p + 1;
                 const uint64_t r = li / a.n_loc;
-                const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
+                const uint64_t wid = r * a.n + shard_map(a).vertex(li - r * a.n_loc);
                 wlo = (uint32_t)wid;
                 whi = (uint32_t)(wid >> 32);
                 const uint32_t x = walks[(uint64_t)p * W + li];
@@ -1840,7 +1840,7 @@ __global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* 
                 li = pr.lp & ((1ull << 56) - 1);
                 pos = (uint32_t)(pr.lp >> 56);
                 const uint64_t r = li / a.n_loc;
-                const uint64_t wid = r * a.n + (a.lo + (li - r * a.n_loc));
+                const uint64_t wid = r * a.n + shard_map(a).vertex(li - r * a.n_loc);
                 wlo = (uint32_t)wid;
                 whi = (uint32_t)(wid >> 32);
                 w.rc = load_rec(a.vrec, pr.cur);
@@ -2931,13 +2931,12 @@ void launch_gather_rows(const uint32_t* walks, uint64_t W, uint32_t L, const uin
 // Index entries of the vertices in the window [v0, v1): sort key
 // (v - v0) << kb | (wid * L + p) (64-bit: n * wpv * L may exceed 2^32),
 // value = the next vertex.  The whole index is the window [0, n).
-__global__ void k_index_entries(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc,
-                                uint64_t lo, int kb, uint32_t v0, uint32_t v1, const uint64_t* __restrict__ col_base,
+__global__ void k_index_entries(const uint32_t* __restrict__ walks, uint64_t W, uint32_t L, ShardMap sm, int kb,
+                                uint32_t v0, uint32_t v1, const uint64_t* __restrict__ col_base,
                                 uint64_t* __restrict__ skeys, uint32_t* __restrict__ vals)
 {
     for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t r = li / n_loc;
-        const uint64_t wid = r * n + lo + (li - r * n_loc);
+        const uint64_t wid = sm.wid(li);
         uint64_t at = col_base[li];
         for (uint32_t p = 0; p < L; p++) {
             const uint32_t v = walks[(uint64_t)p * W + li];
@@ -3013,7 +3012,7 @@ __global__ __launch_bounds__(256) void k_aff_count(const uint8_t* __restrict__ a
 }
 
 __global__ __launch_bounds__(256) void k_aff_write(const uint8_t* __restrict__ aff, uint64_t W, const uint32_t* __restrict__ offs,
-                                                   uint64_t n, uint64_t n_loc, uint64_t lo, uint32_t* __restrict__ out)
+                                                   ShardMap sm, uint32_t* __restrict__ out)
 {
     const uint64_t base = (uint64_t)blockIdx.x * kAffPerBlock + (uint64_t)threadIdx.x * kAffPerThread;
     const uint32_t c = base < W ? aff_count16(aff, W, base) : 0;
@@ -3035,17 +3034,16 @@ __global__ __launch_bounds__(256) void k_aff_write(const uint8_t* __restrict__ a
     const uint64_t end = base + kAffPerThread < W ? base + kAffPerThread : W;
     for (uint64_t l = base; l < end; l++) {
         if (aff[l] == kNoRewalk) continue;
-        const uint64_t r = l / n_loc;
-        out[at++] = (uint32_t)(r * n + lo + (l - r * n_loc));
+        out[at++] = (uint32_t)sm.wid(l);
     }
 }
 
 unsigned aff_blocks(uint64_t W) { return (unsigned)((W + kAffPerBlock - 1) / kAffPerBlock); }
 void launch_aff_count(const uint8_t* aff, uint64_t W, uint32_t* counts, hipStream_t s)
 { if (W) hipLaunchKernelGGL(k_aff_count, aff_blocks(W), 256, 0, s, aff, W, counts); }
-void launch_aff_write(const uint8_t* aff, uint64_t W, const uint32_t* offs, uint64_t n, uint64_t n_loc, uint64_t lo,
-                      uint32_t* out, hipStream_t s)
-{ if (W) hipLaunchKernelGGL(k_aff_write, aff_blocks(W), 256, 0, s, aff, W, offs, n, n_loc, lo, out); }
+void launch_aff_write(const uint8_t* aff, uint64_t W, const uint32_t* offs, const ShardMap& sm, uint32_t* out,
+                      hipStream_t s)
+{ if (W) hipLaunchKernelGGL(k_aff_write, aff_blocks(W), 256, 0, s, aff, W, offs, sm, out); }
 
 __global__ void k_fill_u64(uint64_t* __restrict__ p, uint64_t cnt, uint64_t v)
 {
@@ -3303,10 +3301,10 @@ void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out,
 void launch_walk_lengths(const uint32_t* walks, uint64_t W, uint32_t L, uint32_t v0, uint32_t v1, uint64_t* len,
                          hipStream_t s)
 { hipLaunchKernelGGL(k_walk_lengths, grid_for(W, 256), 256, 0, s, walks, W, L, v0, v1, len); }
-void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, uint64_t n, uint64_t n_loc, uint64_t lo, int kb,
+void launch_index_entries(const uint32_t* walks, uint64_t W, uint32_t L, const ShardMap& sm, int kb,
                           uint32_t v0, uint32_t v1, const uint64_t* col_base, uint64_t* skeys, uint32_t* vals,
                           hipStream_t s)
-{ hipLaunchKernelGGL(k_index_entries, grid_for(W, 256), 256, 0, s, walks, W, L, n, n_loc, lo, kb, v0, v1, col_base, skeys, vals); }
+{ hipLaunchKernelGGL(k_index_entries, grid_for(W, 256), 256, 0, s, walks, W, L, sm, kb, v0, v1, col_base, skeys, vals); }
 void launch_index_split(const uint64_t* skeys, uint64_t E, int kb, unsigned long long* counts, uint64_t* keys, hipStream_t s)
 { hipLaunchKernelGGL(k_index_split, grid_for(E, 256), 256, 0, s, skeys, E, kb, counts, keys); }
 void launch_fill_u64(uint64_t* p, uint64_t cnt, uint64_t v, hipStream_t s)

@@ -29,6 +29,8 @@ Two forms:
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
+
 import numpy as np
 
 
@@ -47,6 +49,48 @@ def balanced_shards(deg: np.ndarray, parts: int):
 def shard_walk_ids(n: int, wpv: int, lo: int, hi: int) -> np.ndarray:
     """Global walk ids of a shard, in its local (export) order: r-major, then v."""
     v = np.arange(lo, hi, dtype=np.int64)
+    return (np.arange(wpv, dtype=np.int64)[:, None] * n + v[None, :]).ravel()
+
+
+@dataclass(frozen=True)
+class BlockShard:
+    """The start vertices of blocks part, part + parts, ... of 2^bits
+    consecutive vertices (WharfMH.set_shard_blocks, include/wharf_gpu.h).
+    Contiguous ranges of an RMAT graph re-walk at rates 10-12 % apart (hub
+    regions vs the rest); dealing 64 Ki-vertex blocks round-robin
+    gives every rank the same mix."""
+    part: int
+    parts: int
+    bits: int
+    n: int
+
+    def blocks(self):
+        B = 1 << self.bits
+        nb = -(-self.n // B)
+        return [(q * B, min(self.n, (q + 1) * B)) for q in range(self.part, nb, self.parts)]
+
+    def size(self) -> int:
+        return sum(b - a for a, b in self.blocks())
+
+    def vertices(self) -> np.ndarray:
+        return np.concatenate([np.arange(a, b, dtype=np.int64) for a, b in self.blocks()] or
+                              [np.zeros(0, dtype=np.int64)])
+
+
+def block_shards(n: int, parts: int, bits: int = 16):
+    return [BlockShard(g, parts, bits, n) for g in range(parts)]
+
+
+def shard_size(shard) -> int:
+    """Start vertices of a shard: a (lo, hi) range or a BlockShard."""
+    return shard.size() if isinstance(shard, BlockShard) else shard[1] - shard[0]
+
+
+def shard_walk_ids_of(shard, n: int, wpv: int) -> np.ndarray:
+    """shard_walk_ids for either kind of shard (local order: r-major, then ascending v)."""
+    if not isinstance(shard, BlockShard):
+        return shard_walk_ids(n, wpv, *shard)
+    v = shard.vertices()
     return (np.arange(wpv, dtype=np.int64)[:, None] * n + v[None, :]).ravel()
 
 
@@ -108,10 +152,29 @@ def local_rows_to_global(lo: int, hi: int, n: int, first: int, count: int):
     return runs
 
 
+def shard_rows_to_global(shard, n: int, first: int, count: int):
+    """local_rows_to_global for either kind of shard: runs of consecutive walk
+    ids (a BlockShard's run also ends at each of its blocks)."""
+    if not isinstance(shard, BlockShard):
+        return local_rows_to_global(shard[0], shard[1], n, first, count)
+    B = 1 << shard.bits
+    own = shard.size()
+    runs, i, end = [], first, first + count
+    while i < end:
+        r, j = divmod(i, own)
+        q, o = divmod(j, B)                      # the part's q-th block, offset o
+        v = (q * shard.parts + shard.part) * B + o
+        c = min(end - i, own - j, B - o)
+        runs.append((i, c, r * n + v))
+        i += c
+    return runs
+
+
 def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per_rank: int, sink=None,
                           root: int | None = None, group=None, device="cpu", dtype=None):
     """Bounded-memory corpus gather: all-gatherv (root None) or gatherv to `root`.
 
+    shards: per rank, a (lo, hi) start-vertex range or a BlockShard;
     read_local(first, count, out): writes this rank's walk-major local rows
         [first, first + count) into the contiguous 2-D tensor `out` ([count, L]);
     sink(chunk, segments): called on every receiving rank once per chunk, with
@@ -126,7 +189,7 @@ def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per
     dtype = dtype or torch.int32
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    owns = [(hi - lo) * wpv for lo, hi in shards]
+    owns = [shard_size(sh) * wpv for sh in shards]
     if len(owns) != world:
         raise ValueError(f"{len(owns)} shards for a world of {world}")
     K = max(1, int(rows_per_rank))
@@ -166,9 +229,9 @@ def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per
             torch.cuda.current_stream(buf.device).synchronize()
         if receives and sink is not None:
             segs = []
-            for g, (lo, hi) in enumerate(shards):
+            for g, sh in enumerate(shards):
                 if cnt[g]:
-                    for lf, k, gf in local_rows_to_global(lo, hi, n, parts[g][0], cnt[g]):
+                    for lf, k, gf in shard_rows_to_global(sh, n, parts[g][0], cnt[g]):
                         segs.append((base[g] + lf - parts[g][0], k, gf))
             sink(buf[:sum(cnt)], segs)
             if cuda:
@@ -199,17 +262,17 @@ def corpus_checksum(rows, global_first: int, L: int, block_rows: int = 1 << 16):
     return total
 
 
-def local_corpus_checksum(read_local, lo: int, hi: int, n: int, wpv: int, L: int, rows_per_call: int,
-                          device="cpu"):
-    """corpus_checksum of this rank's own walks, read chunk by chunk."""
+def local_corpus_checksum(read_local, shard, n: int, wpv: int, L: int, rows_per_call: int, device="cpu"):
+    """corpus_checksum of this rank's own walks (shard: a (lo, hi) range or a
+    BlockShard), read chunk by chunk."""
     import torch
 
-    own = (hi - lo) * wpv
+    own = shard_size(shard) * wpv
     buf = torch.empty((max(1, min(rows_per_call, own)), L), dtype=torch.int32, device=device)
     total = torch.zeros((), dtype=torch.int64, device=device)
     for f in range(0, own, buf.shape[0]):
         k = min(buf.shape[0], own - f)
         read_local(f, k, buf[:k])
-        for lf, c, gf in local_rows_to_global(lo, hi, n, f, k):
+        for lf, c, gf in shard_rows_to_global(shard, n, f, k):
             total += corpus_checksum(buf[lf - f:lf - f + c], gf, L)
     return total

@@ -148,6 +148,26 @@ class WharfMH:
         L.check(L.lib.wharf_set_shard(self._h, lo, hi), self._h, "set_shard")
         self.config.shard_lo, self.config.shard_hi = lo, hi
 
+    def set_shard_blocks(self, part: int, parts: int, block_bits: int = 16) -> None:
+        """Own the walks of the start vertices in blocks part, part + parts, ...
+        of 2^block_bits consecutive vertices (drops current walks): every part
+        gets the same mix of the graph's regions (distributed.BlockShard)."""
+        L.check(L.lib.wharf_set_shard_blocks(self._h, part, parts, block_bits), self._h, "set_shard_blocks")
+        self.config.shard_lo, self.config.shard_hi = 0, 0
+
+    def shard_blocks(self):
+        """(part, parts, block_bits); (0, 1, 0) for a contiguous shard."""
+        a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        L.check(L.lib.wharf_shard_blocks(self._h, C.byref(a), C.byref(b), C.byref(c)), self._h, "shard_blocks")
+        return a.value, b.value, c.value
+
+    def apply_shard(self, shard) -> None:
+        """A shard of distributed.py: a (lo, hi) start-vertex range or a BlockShard."""
+        if isinstance(shard, tuple):
+            self.set_shard(*shard)
+        else:
+            self.set_shard_blocks(shard.part, shard.parts, shard.bits)
+
     @property
     def number_of_walks(self) -> int:
         return self.shard()[2]

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define WHARF_ABI_VERSION 5
+#define WHARF_ABI_VERSION 6
 
 enum {
     WHARF_OK = 0,
@@ -158,6 +158,16 @@ int wharf_shard(const wharf_handle* h, uint64_t* lo, uint64_t* hi, uint64_t* wal
 /* Re-partition the walks: this handle owns the walks of start vertices
  * [lo, hi) (hi == 0: all).  Drops the current walks (like destroy_index). */
 int wharf_set_shard(wharf_handle* h, uint64_t lo, uint64_t hi);
+
+/* Re-partition the walks by vertex blocks: this handle owns the walks of the
+ * start vertices in blocks part, part + parts, part + 2 parts, ... of
+ * 2^block_bits consecutive vertices (6 <= block_bits <= 31).  Every part gets
+ * the same mix of the graph's regions, so the parts' walks re-walk at the same
+ * rate (contiguous ranges of an RMAT graph do not: DESIGN.md §8).  Local walk
+ * order stays ascending in walk id.  Drops the current walks; wharf_set_shard
+ * returns to a contiguous range.  wharf_shard reports lo = 0, hi = n. */
+int wharf_set_shard_blocks(wharf_handle* h, uint32_t part, uint32_t parts, uint32_t block_bits);
+int wharf_shard_blocks(const wharf_handle* h, uint32_t* part, uint32_t* parts, uint32_t* block_bits);
 
 /* flatten_graph (wharfmh.h:175-208): offsets_out n+1 entries, targets_out m
  * (targets_out NULL: offsets only). */

@@ -836,12 +836,16 @@ def test_szudzik_device(W):
     np.testing.assert_array_equal(uy, y)
 
 
+@pytest.mark.parametrize("kind", ["ranges", "blocks"])
 @pytest.mark.parametrize("mode", ["det", "mh_deepwalk", "mh_node2vec"])
-def test_shards_reproduce_the_full_corpus(W, mode):
-    """Walks sharded by start-vertex range (the multi-GPU layout) are bit-identical
-    to the single-handle corpus, through generation and an insert/delete pair."""
-    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards, shard_walk_ids
-    n = 1 << 12
+def test_shards_reproduce_the_full_corpus(W, mode, kind):
+    """Walks sharded by start-vertex range or by vertex blocks dealt round-robin
+    (the multi-GPU layouts) are bit-identical to the single-handle corpus,
+    through generation and an insert/delete pair: walks, walk ids, affected ids,
+    walk() text, the inverted index of each shard's walks; block shards on a
+    graph whose last block is short."""
+    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards, block_shards, shard_walk_ids_of
+    n = 1 << 12 if kind == "ranges" else 4000
     base = O.generate_batch_of_edges(60000, 2 * n, 8, False, False)
     off, adj = O.csr_from_edges(n, base)
     deg = np.diff(off.astype(np.int64))
@@ -855,9 +859,13 @@ def test_shards_reproduce_the_full_corpus(W, mode):
     fw1 = full.walks()
     fa2 = full.delete_edges_batch(b, remove_dups=True).copy()
     fw2 = full.walks()
-    for lo, hi in balanced_shards(deg, 3):
-        g = W.WharfMH.from_csr(off, adj, config=W.WharfConfig(shard_lo=lo, shard_hi=hi, **kw))
-        ids = shard_walk_ids(n, 3, lo, hi)
+    shards = balanced_shards(deg, 3) if kind == "ranges" else block_shards(n, 3, 6)
+    seen = []
+    for sh in shards:
+        g = W.WharfMH.from_csr(off, adj, config=W.WharfConfig(**kw))
+        g.apply_shard(sh)
+        ids = shard_walk_ids_of(sh, n, 3)
+        seen.append(ids)
         np.testing.assert_array_equal(g.walk_ids(), ids)
         g.generate_initial_random_walks()
         np.testing.assert_array_equal(g.walks(), fw0[ids])
@@ -867,9 +875,15 @@ def test_shards_reproduce_the_full_corpus(W, mode):
         a2 = g.delete_edges_batch(b, remove_dups=True)
         np.testing.assert_array_equal(np.sort(a2), np.intersect1d(fa2, ids))
         np.testing.assert_array_equal(g.walks(), fw2[ids])
+        for i in (0, len(ids) // 2, len(ids) - 1):
+            assert g.walk(int(ids[i])) == O.walk_string(fw2[ids[i]])
         with pytest.raises(RuntimeError):
             g.walk(int(np.setdiff1d(np.arange(3 * n), ids)[0]))   # not owned by this shard
+        c, k, nx = g.inverted_index()
+        keys = (ids[:, None] * 30 + np.arange(30)[None, :])[fw2[ids] != W.SENTINEL]
+        assert int(c.sum()) == len(keys) and np.array_equal(np.sort(k), np.sort(keys.astype(np.uint64)))
         g.destroy()
+    assert np.array_equal(np.sort(np.concatenate(seen)), np.arange(3 * n))
     full.destroy()
 
 

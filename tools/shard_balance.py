@@ -30,10 +30,12 @@ def main():
     ap.add_argument("--batches", type=int, default=3)
     ap.add_argument("--mixed", action="store_true")
     ap.add_argument("--shards", default="", help="comma list of shard indices (default: all)")
+    ap.add_argument("--blocks", type=int, default=0,
+                    help="block shards of 2^BLOCKS vertices dealt round-robin (0: contiguous balanced ranges)")
     a = ap.parse_args()
     import torch
     import dynamicgraphrepresentationlearning_amd as W
-    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards
+    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards, block_shards, shard_size
     n = 1 << a.scale
     cfg = W.WharfConfig(walks_per_vertex=a.wpv, walk_length=80, deterministic=False, seed=0x5EED,
                         model=W.NODE2VEC if a.model == "node2vec" else W.DEEPWALK, paramP=0.5, paramQ=2.0)
@@ -44,9 +46,9 @@ def main():
         t0 = time.time()
         g = W.WharfMH.from_rmat(n, a.samples, 2 * n, seed=4, config=cfg)
         if shards is None:
-            shards = balanced_shards(np.diff(g.offsets().astype(np.int64)), a.parts)
-        lo, hi = shards[i]
-        g.set_shard(lo, hi)
+            shards = block_shards(n, a.parts, a.blocks) if a.blocks else \
+                balanced_shards(np.diff(g.offsets().astype(np.int64)), a.parts)
+        g.apply_shard(shards[i])
         g.generate_initial_random_walks()
         first = g.stats()["last_walk_kernel_ms"]
         g.generate_initial_random_walks()
@@ -64,7 +66,7 @@ def main():
                 rec["walk"].append(st["last_walk_update_ms"])
                 rec["steps"].append(st["steps"])
                 rec["affected"].append(st["affected"])
-        r = {"shard": i, "range": [int(lo), int(hi)], "walks": g.number_of_walks,
+        r = {"shard": i, "shard_def": str(shards[i]), "walks": g.number_of_walks,
              "first_generation_ms": round(first, 2), "generation_ms": round(gen["last_walk_kernel_ms"], 2),
              "generation_steps": gen["steps"],
              "batch_median_ms": round(float(np.median(rec["ms"])), 3),
@@ -81,7 +83,9 @@ def main():
     w = [r["walk_update_median_ms"] for r in res]
     gen = [r["generation_ms"] for r in res]
     print(json.dumps({"summary": True, "config": f"RMAT scale {a.scale}, {a.samples} samples (seed 4), {a.model} MH, "
-                                                 f"wpv {a.wpv}, {a.parts} shards, {a.batches} batches"
+                                                 f"wpv {a.wpv}, {a.parts} shards "
+                                                 f"({'blocks of 2^%d' % a.blocks if a.blocks else 'ranges'}), "
+                                                 f"{a.batches} batches"
                                                  f"{' (insert+delete)' if a.mixed else ''}",
                       "batch_median_ms_max": max(b), "batch_median_ms_min": min(b),
                       "batch_max_over_min": round(max(b) / min(b), 3),
