@@ -513,8 +513,9 @@ def per_gpu_of_8(args, W, torch, dev, barrier):
     wpv 10 (the survey's 656 M walks / 8), mixed insert/delete batches.  The
     graphs use seed 4 (tools/bigscale.py).  Each case is skipped with its error
     when the device cannot hold it, so the headline line always prints."""
-    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards
-    out = {"note": "one GPU running the work one rank of an 8-GPU job does; graphs built on the device (seed 4)"}
+    from dynamicgraphrepresentationlearning_amd.distributed import block_shards
+    out = {"note": "one GPU running the work one rank of an 8-GPU job does (the job's block shard 0 of 8: "
+                   "2^16-vertex blocks dealt round-robin, as multi_gpu_job); graphs built on the device (seed 4)"}
     cases = [("configs3_deepwalk_mh_shard0of8", 25, 1_200_000_000, W.DEEPWALK, False, 8, False),
              ("configs3_deepwalk_det_shard0of8", 25, 1_200_000_000, W.DEEPWALK, True, 8, False),
              ("configs3_deepwalk_mh_all_walks_1gpu", 25, 1_200_000_000, W.DEEPWALK, False, 1, False),
@@ -527,9 +528,8 @@ def per_gpu_of_8(args, W, torch, dev, barrier):
             cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, model=model, paramP=0.5, paramQ=2.0,
                                 deterministic=det, seed=0x5EED)
             g = W.WharfMH.from_rmat(n, samples, 2 * n, seed=4, config=cfg, device=dev)
-            deg = np.diff(g.offsets().astype(np.int64))
-            lo, hi = balanced_shards(deg, parts)[0]
-            g.set_shard(lo, hi)
+            sh = block_shards(n, parts, 16)[0]
+            g.apply_shard(sh)
             build_s = time.time() - t0
             g.generate_initial_random_walks()
             first = g.stats()
@@ -540,7 +540,7 @@ def per_gpu_of_8(args, W, torch, dev, barrier):
             rec = {"graph": f"RMAT scale {scale}, {samples} undirected samples (seed 4), m={g.number_of_edges()}",
                    "model": f"{'node2vec p=0.5 q=2 WEIGHT' if model == W.NODE2VEC else 'DeepWalk'} "
                             f"{'deterministic' if det else 'MH'}, walks_per_vertex=10, L=80",
-                   "walks": g.number_of_walks, "shard": [int(lo), int(hi)], "of": parts, "build_s": round(build_s, 1),
+                   "walks": g.number_of_walks, "shard": str(sh), "of": parts, "build_s": round(build_s, 1),
                    "first_generation_ms": round(first["last_walk_kernel_ms"], 2),
                    "first_generation_anchor_inits": first["last_anchor_inits"],
                    "generation_ms": round(warm["last_walk_kernel_ms"], 2),
