@@ -45,10 +45,6 @@ struct WharfError : std::runtime_error {
         if (!(cond)) throw WharfError((code), (msg));   \
     } while (0)
 
-struct LastNonzero {   // associative: the scan carries the last nonzero value
-    __host__ __device__ uint32_t operator()(uint32_t x, uint32_t y) const { return y ? y : x; }
-};
-
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -1365,11 +1361,18 @@ int wharf_generate(wharf_handle* h)
         h->st_park_passes = 0;
         WalkArgs a = h->walk_args();
         HIPCHK(hipEventRecord(h->ev[0], h->s));
-        // node2vec MH with a cold anchor cache and many more steps than states:
-        // every anchor computed up front (k_anchor_init_all), timed with the generation
+        // node2vec MH with a cold anchor cache and at least as many steps as states
+        // (slots): every anchor computed up front (k_anchor_init_all), timed with the
+        // generation.  Round 4: the rule was 4 steps per slot; at configs[4]'s 1/8 shard
+        // (1.6 per slot) the lazy generation leaves 1.1 G of 3.6 G states cold, and every
+        // update's re-walk then runs into them: 88.5 M inits per batch, re-walk 65.5 ms,
+        // against 9.4 M and 34.9 ms with all anchors computed (first generation 1.06 ->
+        // 2.08 s; profiles/r04/preinit_all).  WHARF_PREINIT_ALL=1 / 0 forces it on / off.
         const char* no_pre = getenv("WHARF_NO_PREINIT");
-        if (a.model == kNode2Vec && !a.det && a.anchor && h->anchors_cold && h->pool_used &&
-            (uint64_t)h->W * (h->L - 1) >= 4 * h->pool_used && !(no_pre && atoi(no_pre))) {
+        const char* pre_all = getenv("WHARF_PREINIT_ALL");
+        const bool all_rule = pre_all && *pre_all ? atoi(pre_all) != 0 : (uint64_t)h->W * (h->L - 1) >= h->pool_used;
+        if (a.model == kNode2Vec && !a.det && a.anchor && h->anchors_cold && h->pool_used && all_rule &&
+            !(no_pre && atoi(no_pre))) {
             size_t free_b = 0, total_b = 0;
             HIPCHK(hipMemGetInfo(&free_b, &total_b));
             if (h->pool_used * 4 + (1ull << 30) < free_b) {
@@ -1377,10 +1380,7 @@ int wharf_generate(wharf_handle* h)
                 owner.ensure(h->pool_used * 4);
                 uint32_t* ow = owner.as<uint32_t>();
                 HIPCHK(hipMemsetAsync(ow, 0, h->pool_used * 4, h->s));
-                launch_slot_owner_marks(h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->n, ow, h->s);
-                h->rp([&](void* t, size_t& b) {   // last nonzero mark: the owner of every slot
-                    return rocprim::inclusive_scan(t, b, ow, ow, (size_t)h->pool_used, LastNonzero{}, h->s);
-                });
+                launch_slot_owner_fill(h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->n, ow, h->s);
                 launch_anchor_init_all(a, ow, h->pool_used, h->s);
                 HIPCHK(hipStreamSynchronize(h->s));   // before the owner buffer is released
                 owner.release();

@@ -94,7 +94,7 @@ void launch_park_init(const WalkArgs& a, const void* in, const unsigned long lon
 void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStream_t s);
 void launch_source_degrees(const RunInfo* runs, uint64_t k, const ERec* vrec, uint64_t* out, hipStream_t s);
 void launch_anchor_preinit(const WalkArgs& a, const uint64_t* preoff, uint64_t k, hipStream_t s);
-void launch_slot_owner_marks(const uint64_t* off, const uint32_t* deg, uint64_t n, uint32_t* owner, hipStream_t s);
+void launch_slot_owner_fill(const uint64_t* off, const uint32_t* deg, uint64_t n, uint32_t* owner, hipStream_t s);
 void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t slots, hipStream_t s);
 void launch_vrec(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* row_epoch, ERec* vrec,
                  hipStream_t s);

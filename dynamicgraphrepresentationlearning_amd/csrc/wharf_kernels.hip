@@ -637,14 +637,20 @@ __global__ __launch_bounds__(256) void k_anchor_preinit(WalkArgs a, const uint64
 // lazily each first entry stalls its lock-step wave for an init.  Instead the
 // anchors of all slots are computed up front, one lane per slot, every lane of
 // a wave initialising; the same pure function of the snapshot, so the corpus
-// is unchanged.  owner[e] = (row owner of slot e) + 1, from the row starts by
-// a last-nonzero scan (k_slot_owner_marks + the host's scan); slack slots hold
-// kGap and are skipped.
-__global__ void k_slot_owner_marks(const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg, uint64_t n,
-                                   uint32_t* __restrict__ owner)
+// is unchanged.  owner[e] = (row owner of slot e) + 1, written row by row (one
+// wave per row, lanes over its slots: no scan over the pool, whose ~4.1 G slots
+// at configs[4] are past 2^31); slack slots keep 0 and are skipped.
+__global__ __launch_bounds__(256) void k_slot_owner_fill(const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ deg, uint64_t n,
+                                                         uint32_t* __restrict__ owner)
 {
-    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
-        if (deg[v]) owner[off[v]] = (uint32_t)v + 1;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t v = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); v < n; v += waves) {
+        const uint64_t o = off[v];
+        const uint32_t d = deg[v];
+        for (uint32_t i = lane; i < d; i += 64) owner[o + i] = (uint32_t)v + 1;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint32_t* __restrict__ owner, uint64_t slots)
@@ -667,9 +673,9 @@ __global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint3
     wave_add(a.counters + 7, inits);
 }
 
-void launch_slot_owner_marks(const uint64_t* off, const uint32_t* deg, uint64_t n, uint32_t* owner, hipStream_t s)
+void launch_slot_owner_fill(const uint64_t* off, const uint32_t* deg, uint64_t n, uint32_t* owner, hipStream_t s)
 {
-    if (n) hipLaunchKernelGGL(k_slot_owner_marks, grid_for(n, 256), 256, 0, s, off, deg, n, owner);
+    if (n) hipLaunchKernelGGL(k_slot_owner_fill, cu_count() * 32, 256, 0, s, off, deg, n, owner);
 }
 
 void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t slots, hipStream_t s)

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--samples", type=int, default=1_200_000_000)
     ap.add_argument("--model", default="deepwalk")
     ap.add_argument("--wpv", type=int, default=10)
+    ap.add_argument("--p", type=float, default=0.5)
+    ap.add_argument("--q", type=float, default=2.0)
     ap.add_argument("--parts", type=int, default=8)
     ap.add_argument("--batches", type=int, default=3)
     ap.add_argument("--mixed", action="store_true")
@@ -38,7 +40,7 @@ def main():
     from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards, block_shards, shard_size
     n = 1 << a.scale
     cfg = W.WharfConfig(walks_per_vertex=a.wpv, walk_length=80, deterministic=False, seed=0x5EED,
-                        model=W.NODE2VEC if a.model == "node2vec" else W.DEEPWALK, paramP=0.5, paramQ=2.0)
+                        model=W.NODE2VEC if a.model == "node2vec" else W.DEEPWALK, paramP=a.p, paramQ=a.q)
     which = [int(x) for x in a.shards.split(",")] if a.shards else list(range(a.parts))
     shards = None
     res = []
@@ -50,11 +52,12 @@ def main():
                 balanced_shards(np.diff(g.offsets().astype(np.int64)), a.parts)
         g.apply_shard(shards[i])
         g.generate_initial_random_walks()
-        first = g.stats()["last_walk_kernel_ms"]
+        first_st = g.stats()
+        first = first_st["last_walk_kernel_ms"]
         g.generate_initial_random_walks()
         gen = g.stats()
         ids = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device="cuda:0")
-        rec = {k: [] for k in ("ms", "graph", "walk", "steps", "affected")}
+        rec = {k: [] for k in ("ms", "graph", "walk", "steps", "affected", "inits")}
         for b in range(a.batches):
             batch = W.generate_batch_of_edges(5000, n, b, False, False)
             for ins in ((True, False) if a.mixed else (True,)):
@@ -66,13 +69,15 @@ def main():
                 rec["walk"].append(st["last_walk_update_ms"])
                 rec["steps"].append(st["steps"])
                 rec["affected"].append(st["affected"])
+                rec["inits"].append(st["last_anchor_inits"])
         r = {"shard": i, "shard_def": str(shards[i]), "walks": g.number_of_walks,
              "first_generation_ms": round(first, 2), "generation_ms": round(gen["last_walk_kernel_ms"], 2),
-             "generation_steps": gen["steps"],
+             "generation_steps": gen["steps"], "first_generation_anchor_inits": first_st["last_anchor_inits"],
              "batch_median_ms": round(float(np.median(rec["ms"])), 3),
              "graph_update_median_ms": round(float(np.median(rec["graph"])), 3),
              "walk_update_median_ms": round(float(np.median(rec["walk"])), 3),
              "rewalk_steps_mean": int(np.mean(rec["steps"])), "affected_mean": int(np.mean(rec["affected"])),
+             "anchor_inits_mean": int(np.mean(rec["inits"])), "batch_ms": [round(x, 2) for x in rec["ms"]],
              "rewalk_Gsteps_per_s": round(float(np.sum(rec["steps"]) / np.sum(rec["walk"]) / 1e6), 2),
              "wall_s": round(time.time() - t0, 1)}
         print(json.dumps(r), flush=True)
