@@ -237,6 +237,8 @@ struct wharf_handle {
     const uint32_t* staged_row(uint64_t li)
     {
         if (last_aff_version != walks_version || last_aff.empty()) return nullptr;
+        const char* ns = getenv("WHARF_WALK_NO_STAGE");   // A/B (tools/walk_readout)
+        if (ns && atoi(ns)) return nullptr;
         if (stage_version != walks_version) {
             // stage only when li is one of them (a reader of other walks never pays for it)
             const uint64_t wid = smap().wid(li);

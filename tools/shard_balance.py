@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--parts", type=int, default=8)
     ap.add_argument("--batches", type=int, default=3)
     ap.add_argument("--mixed", action="store_true")
-    ap.add_argument("--shards", default="", help="comma list of shard indices (default: all)")
+    ap.add_argument("--shards", type=int, nargs="*", default=None, help="shard indices (default: all)")
     ap.add_argument("--blocks", type=int, default=0,
                     help="block shards of 2^BLOCKS vertices dealt round-robin (0: contiguous balanced ranges)")
     a = ap.parse_args()
@@ -41,7 +41,7 @@ def main():
     n = 1 << a.scale
     cfg = W.WharfConfig(walks_per_vertex=a.wpv, walk_length=80, deterministic=False, seed=0x5EED,
                         model=W.NODE2VEC if a.model == "node2vec" else W.DEEPWALK, paramP=a.p, paramQ=a.q)
-    which = [int(x) for x in a.shards.split(",")] if a.shards else list(range(a.parts))
+    which = a.shards if a.shards else list(range(a.parts))
     shards = None
     res = []
     for i in which:

@@ -6,9 +6,12 @@
 // Then the reference's incremental pattern (vertex-classification.cpp:171-176):
 // after each insert batch of the throughput driver's sizes (5 / 50 / 500
 // directed edges between low-degree vertices, throughput-latency.cpp:87-93), walk(i) of the affected
-// walks only — with the snapshot chunk taken once 32 of its walks were read
-// (default), taken on the first read (WHARF_WALK_FILL_AFTER=0, round 3), and a
-// device read per call.
+// walks only, each mode after a batch of its own (same size, its own edges): the
+// default (all the update's affected rows gathered with one list gather on the
+// first read of one of them, round 4), without that stage (WHARF_WALK_NO_STAGE=1:
+// the snapshot chunk taken once 32 of its walks were read, single rows before),
+// the chunk taken on the first read (+ WHARF_WALK_FILL_AFTER=0, round 3), and a
+// device read per call (WHARF_WALK_NO_SNAPSHOT=1).
 //
 //   tools/walk_readout [n_old=20000] [n_new=41943040]
 #include <chrono>
@@ -61,43 +64,41 @@ int main(int argc, char** argv)
     std::vector<uint32_t> aff(W), pairs;
     std::string sparse = "[";
     for (uint64_t bs : {5ull, 50ull, 500ull}) {
-        // edges between low-degree vertices (RMAT's upper id half), so the affected walks are a
-        // sparse set: an RMAT batch of any size touches hubs that most walks visit
-        pairs.assign(2 * bs, 0);
-        uint64_t cnt = bs, naff = 0, x = 88172645463325252ull + bs;
-        for (uint64_t i = 0; i < 2 * bs; i++) {
-            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
-            pairs[i] = (uint32_t)(n / 2 + x % (n / 2));
-        }
-        if (wharf_insert_edges(h, cnt, pairs.data(), WHARF_REMOVE_DUPS | WHARF_APPLY_WALK_UPDATES, aff.data(), &naff))
-            return 4;
-        printf("batch of %llu edges: %llu affected walks\n", (unsigned long long)cnt, (unsigned long long)naff);
-        fflush(stdout);
-        const char* modes[3][2] = {{"fill_after_32", nullptr}, {"fill_on_first_read", "0"}, {"device_read_per_call", nullptr}};
-        std::string rec = "{\"batch_edges\": " + std::to_string(cnt) + ", \"affected\": " + std::to_string(naff);
-        for (int m = 0; m < 3; m++) {
-            // a fresh snapshot per mode: one tiny update that changes no walk would not invalidate it,
-            // so re-set the walks' version through the library's own rule (an empty walk update)
-            uint32_t none = 0;
-            uint64_t dummy = 0;
-            if (wharf_batch_walk_update(h, &none, 0, 0, nullptr, &dummy)) return 5;
-            if (m == 1) setenv("WHARF_WALK_FILL_AFTER", "0", 1);
-            if (m == 2) setenv("WHARF_WALK_NO_SNAPSHOT", "1", 1);
+        const char* modes[4] = {"default_stage", "no_stage_fill_after_32", "no_stage_fill_on_first_read",
+                                "device_read_per_call"};
+        std::string rec = "{\"batch_edges\": " + std::to_string(bs);
+        for (int m = 0; m < 4; m++) {
+            // edges between low-degree vertices (RMAT's upper id half), so the affected walks are a
+            // sparse set: an RMAT batch of any size touches hubs that most walks visit
+            pairs.assign(2 * bs, 0);
+            uint64_t cnt = bs, naff = 0, x = 88172645463325252ull + bs * 7 + (uint64_t)m;
+            for (uint64_t i = 0; i < 2 * bs; i++) {
+                x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                pairs[i] = (uint32_t)(n / 2 + x % (n / 2));
+            }
+            if (wharf_insert_edges(h, cnt, pairs.data(), WHARF_REMOVE_DUPS | WHARF_APPLY_WALK_UPDATES, aff.data(), &naff))
+                return 4;
+            if (m >= 1) setenv("WHARF_WALK_NO_STAGE", "1", 1);
+            if (m == 2) setenv("WHARF_WALK_FILL_AFTER", "0", 1);
+            if (m == 3) setenv("WHARF_WALK_NO_SNAPSHOT", "1", 1);
             t0 = now();
             for (uint64_t i = 0; i < naff; i++) {
                 if (wharf_walk_string(h, aff[i], buf.data(), buf.size(), &len)) return 6;
                 total += len;
             }
             const double t = now() - t0;
+            unsetenv("WHARF_WALK_NO_STAGE");
+            unsetenv("WHARF_WALK_FILL_AFTER");
             unsetenv("WHARF_WALK_NO_SNAPSHOT");
-            char part[160];
-            snprintf(part, sizeof part, ", \"%s_ms\": %.3f", modes[m][0], 1e3 * t);
+            char part[200];
+            snprintf(part, sizeof part, ", \"%s\": {\"affected\": %llu, \"ms\": %.3f}", modes[m],
+                     (unsigned long long)naff, 1e3 * t);
             rec += part;
-            printf("  %s: %.3f ms\n", modes[m][0], 1e3 * t);
+            printf("batch of %llu edges, %s: %llu affected walks read in %.3f ms\n", (unsigned long long)bs, modes[m],
+                   (unsigned long long)naff, 1e3 * t);
             fflush(stdout);
         }
         sparse += (sparse.size() > 1 ? ", " : "") + rec + "}";
-        unsetenv("WHARF_WALK_FILL_AFTER");
     }
     sparse += "]";
     printf("{\"walks\": %llu, \"per_call_device_read\": {\"calls\": %llu, \"seconds\": %.3f, \"us_per_call\": %.2f, "
