@@ -1369,7 +1369,7 @@ int wharf_generate(wharf_handle* h)
         // (1.6 per slot) the lazy generation leaves 1.1 G of 3.6 G states cold, and every
         // update's re-walk then runs into them: 88.5 M inits per batch, re-walk 65.5 ms,
         // against 9.4 M and 34.9 ms with all anchors computed (first generation 1.06 ->
-        // 2.08 s; profiles/r04/preinit_all).  WHARF_PREINIT_ALL=1 / 0 forces it on / off.
+        // 1.10 s; profiles/r04/preinit_all).  WHARF_PREINIT_ALL=1 / 0 forces it on / off.
         const char* no_pre = getenv("WHARF_NO_PREINIT");
         const char* pre_all = getenv("WHARF_PREINIT_ALL");
         const bool all_rule = pre_all && *pre_all ? atoi(pre_all) != 0 : (uint64_t)h->W * (h->L - 1) >= h->pool_used;

@@ -63,6 +63,16 @@ int main(int argc, char** argv)
     // sparse: the affected walks of small batches
     std::vector<uint32_t> aff(W), pairs;
     std::string sparse = "[";
+    {   // the first read after an update drops the full readout's pinned chunks (all but four):
+        // paid here once, not by the first mode below
+        uint32_t e[2] = {(uint32_t)(n - 1), (uint32_t)(n - 2)};
+        uint64_t na = 0;
+        if (wharf_insert_edges(h, 1, e, WHARF_REMOVE_DUPS | WHARF_APPLY_WALK_UPDATES, aff.data(), &na)) return 4;
+        t0 = now();
+        if (wharf_walk_string(h, 0, buf.data(), buf.size(), &len)) return 6;
+        printf("first read after the full readout (releases its pinned chunks): %.3f ms\n", 1e3 * (now() - t0));
+        fflush(stdout);
+    }
     for (uint64_t bs : {5ull, 50ull, 500ull}) {
         const char* modes[4] = {"default_stage", "no_stage_fill_after_32", "no_stage_fill_on_first_read",
                                 "device_read_per_call"};
