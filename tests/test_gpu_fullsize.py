@@ -44,6 +44,19 @@ def torch():
     return torch
 
 
+@pytest.fixture(autouse=True)
+def _release_device_memory(torch):
+    """Each full-size case needs most of the 288 GB: handles and tensors left by
+    the previous one (a failed case's handle waits for the collector, torch keeps
+    its cache) are released before the next starts."""
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
+    yield
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
 def _dev_walks(torch, g):
     t = torch.empty((L, g.number_of_walks), dtype=torch.int32, device="cuda:0")
     g.export_walks_device(t.data_ptr(), layout="position")
