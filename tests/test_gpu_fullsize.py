@@ -349,6 +349,33 @@ def _all_edges_csr(torch, doff, dadj, u, v):
     return bool(((lo < end) & (dadj[lo.clamp(max=last)].long() == v)).all())
 
 
+def _all_edges_host(off, adj, u, v):
+    """_all_edges_csr on the host arrays (when the card has no room for a CSR copy)."""
+    u, v = np.asarray(u, dtype=np.int64), np.asarray(v, dtype=np.int64)
+    lo, end = off[u].astype(np.int64), off[u + 1].astype(np.int64)
+    hi = end.copy()
+    last = len(adj) - 1
+    while True:
+        act = lo < hi
+        if not act.any():
+            break
+        mid = (lo + hi) // 2
+        less = adj[np.minimum(mid, last)].astype(np.int64) < v
+        lo = np.where(act & less, mid + 1, lo)
+        hi = np.where(act & ~less, mid, hi)
+    return bool(((lo < end) & (adj[np.minimum(lo, last)].astype(np.int64) == v)).all())
+
+
+def _edge_check(torch, off, adj):
+    """Transition checker against the CSR (off, adj): on a device copy when the card
+    has room for it beside the handle, else on the host arrays."""
+    free, _ = torch.cuda.mem_get_info()
+    if free > off.nbytes + adj.nbytes + (4 << 30):
+        doff, dadj = _csr_dev(torch, off, adj)
+        return lambda u, v: _all_edges_csr(torch, doff, dadj, u, v)
+    return lambda u, v: _all_edges_host(off, adj, u.cpu().numpy(), v.cpu().numpy())
+
+
 def test_configs4_full_size_shard_of_8(W, torch):
     """configs[4]'s per-GPU work of its 8-GPU run at full graph size: the
     friendster-sized RMAT graph (scale 26, 1.8 G undirected samples, ~3.6 G CSR
@@ -410,10 +437,10 @@ def test_configs4_full_size_shard_of_8(W, torch):
         affected = p < L
         assert torch.equal(aff.long(), start[affected])        # wpv 1: walk id = start vertex
         del doff, dadj
+        check = None
         torch.cuda.empty_cache()
         o2, a2 = g.flatten_graph()
-        doff, dadj = _csr_dev(torch, o2, a2)
-        del o2, a2
+        check = _edge_check(torch, o2, a2)
         walked = 0
         for pos in range(L):
             kept = pos <= p
@@ -421,8 +448,8 @@ def test_configs4_full_size_shard_of_8(W, torch):
             if pos + 1 < L:
                 m = affected & (pos >= p) & (after[pos + 1] != sent)
                 walked += int(m.sum())
-                assert _all_edges_csr(torch, doff, dadj, after[pos, m], after[pos + 1, m]), \
-                    f"non-edge re-walk step at {pos}"
+                assert check(after[pos, m], after[pos + 1, m]), f"non-edge re-walk step at {pos}"
         assert walked == steps
         before = after
+        doff = dadj = None
     g.destroy()
