@@ -1375,12 +1375,16 @@ int wharf_generate(wharf_handle* h)
         const bool all_rule = pre_all && *pre_all ? atoi(pre_all) != 0 : (uint64_t)h->W * (h->L - 1) >= h->pool_used;
         if (a.model == kNode2Vec && !a.det && a.anchor && h->anchors_cold && h->pool_used && all_rule &&
             !(no_pre && atoi(no_pre))) {
+            // the slot owners live in the walk matrix, which this generation overwrites next:
+            // the rule (>= 1 step per slot) makes it the larger (W * L > pool_used); a 16-GB
+            // allocation here (configs[4]) cost 0-1 s of page mapping, box to box
             size_t free_b = 0, total_b = 0;
-            HIPCHK(hipMemGetInfo(&free_b, &total_b));
-            if (h->pool_used * 4 + (1ull << 30) < free_b) {
+            const bool in_walks = h->walks.cap >= h->pool_used * 4;
+            if (!in_walks) HIPCHK(hipMemGetInfo(&free_b, &total_b));
+            if (in_walks || h->pool_used * 4 + (1ull << 30) < free_b) {
                 DevBuf owner;
-                owner.ensure(h->pool_used * 4);
-                uint32_t* ow = owner.as<uint32_t>();
+                if (!in_walks) owner.ensure(h->pool_used * 4);
+                uint32_t* ow = in_walks ? h->walks.as<uint32_t>() : owner.as<uint32_t>();
                 HIPCHK(hipMemsetAsync(ow, 0, h->pool_used * 4, h->s));
                 launch_slot_owner_fill(h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->n, ow, h->s);
                 launch_anchor_init_all(a, ow, h->pool_used, h->s);
