@@ -14,6 +14,7 @@
 // device read per call (WHARF_WALK_NO_SNAPSHOT=1).
 //
 //   tools/walk_readout [n_old=20000] [n_new=41943040]
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -88,6 +89,11 @@ int main(int argc, char** argv)
             }
             if (wharf_insert_edges(h, cnt, pairs.data(), WHARF_REMOVE_DUPS | WHARF_APPLY_WALK_UPDATES, aff.data(), &naff))
                 return 4;
+            {   // untimed: one read of an unaffected walk releases the previous mode's pinned chunks
+                uint32_t w = 0;
+                while (std::binary_search(aff.begin(), aff.begin() + naff, w)) w++;
+                if (wharf_walk_string(h, w, buf.data(), buf.size(), &len)) return 6;
+            }
             if (m >= 1) setenv("WHARF_WALK_NO_STAGE", "1", 1);
             if (m == 2) setenv("WHARF_WALK_FILL_AFTER", "0", 1);
             if (m == 3) setenv("WHARF_WALK_NO_SNAPSHOT", "1", 1);
