@@ -775,7 +775,11 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
     const uint32_t L = a.L;
     for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += stride) {
         const uint64_t r = li / a.n_loc;
+#ifdef WHARF_AB_SWEEP_OLD_MAP
+        const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
+#else
         const uint32_t v = (uint32_t)shard_map(a).vertex(li - r * a.n_loc);
+#endif
         const uint64_t wid = r * a.n + v;
         const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
         const uint64_t* __restrict__ rt = DET ? a.rtab + r * L : nullptr;
