@@ -111,7 +111,6 @@ struct ShardMap {
     uint32_t part, parts, bits;
     __host__ __device__ __forceinline__ uint64_t vertex(uint64_t j) const
     {
-        if (parts == 1) return lo + j;   // (a uniform branch: the contiguous case stays one add)
         return lo + ((((j >> bits) * parts + part) << bits) | (j & ((1ull << bits) - 1)));
     }
     __host__ __device__ __forceinline__ uint64_t wid(uint64_t li) const

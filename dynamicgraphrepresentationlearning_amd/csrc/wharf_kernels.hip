@@ -702,7 +702,21 @@ void launch_anchor_preinit(const WalkArgs& a, const uint64_t* preoff, uint64_t k
 
 // Generation (wharfmh.h:275-326): every lane of a wave writes the same
 // position at the same time -> one contiguous 256-B store per step.
-template <int MODEL, bool DET>
+// BLK: the handle holds a block shard (ShardMap); a contiguous one maps j -> lo + j
+// in its own instantiation, which compiles to round 3's code (the generic map in
+// the sweep's prologue changed its loop's code layout: configs[2] re-walk 43.4 ->
+// 48.6 ms on one box, profiles/r04/sweep_map/)
+template <bool BLK>
+__device__ __forceinline__ uint32_t start_vertex(const WalkArgs& a, uint64_t j)
+{
+    if constexpr (BLK) {   // 32-bit: set_shard_blocks requires n * wpv < 2^32
+        const uint32_t jj = (uint32_t)j, b = a.sh_bits;
+        return (uint32_t)a.lo + ((((jj >> b) * a.sh_parts + a.sh_part) << b) | (jj & ((1u << b) - 1u)));
+    }
+    return (uint32_t)(a.lo + j);
+}
+
+template <int MODEL, bool DET, bool BLK = false>
 __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
 {
     uint32_t steps = 0, accepts = 0, inits = 0;
@@ -711,7 +725,7 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
     const uint64_t W = a.W;
     for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += stride) {
         const uint64_t r = li / a.n_loc;
-        const uint32_t v = (uint32_t)shard_map(a).vertex(li - r * a.n_loc);
+        const uint32_t v = start_vertex<BLK>(a, li - r * a.n_loc);
         const uint64_t wid = r * a.n + v;
         const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
         const uint64_t* __restrict__ rt = DET ? a.rtab + r * a.L : nullptr;
@@ -763,7 +777,7 @@ __device__ __forceinline__ bool is_source(const WalkArgs& a, const uint32_t* s_b
     return (a.bitmap[x >> 5] >> (x & 31)) & 1u;
 }
 
-template <int MODEL, bool DET>
+template <int MODEL, bool DET, bool BLK = false>
 __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
 {
     __shared__ uint32_t s_bloom[kBloomWords];
@@ -775,11 +789,10 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
     const uint32_t L = a.L;
     for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += stride) {
         const uint64_t r = li / a.n_loc;
-#ifdef WHARF_AB_SWEEP_OLD_MAP
-        const uint32_t v = (uint32_t)(a.lo + (li - r * a.n_loc));
-#else
-        const uint32_t v = (uint32_t)shard_map(a).vertex(li - r * a.n_loc);
-#endif
+        // the start vertex: the walk's position 0 (no re-walk moves it) under a block
+        // shard; lo + j otherwise (round 3's code: the generic map in this prologue changed
+        // the loop's code layout, configs[2] re-walk 43.4 -> 48.6 ms, profiles/r04/sweep_map/)
+        const uint32_t v = BLK ? walks[li] : start_vertex<false>(a, li - r * a.n_loc);
         const uint64_t wid = r * a.n + v;
         const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
         const uint64_t* __restrict__ rt = DET ? a.rtab + r * L : nullptr;
@@ -1613,7 +1626,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
             li = ent & ((1ull << 56) - 1);
             p = (uint32_t)(ent >> 56);
             const uint64_t r = li / a.n_loc;
-            const uint64_t wid = r * a.n + shard_map(a).vertex(li - r * a.n_loc);
+            const uint64_t wid = r * a.n + a.walks[li];
             wlo = (uint32_t)wid;
             whi = (uint32_t)(wid >> 32);
             if constexpr (DET) rt = a.rtab + r * L;
@@ -1690,7 +1703,7 @@ __global__ __launch_bounds__(256) void k_rewalk_block(WalkArgs a)
             li = ent & ((1ull << 56) - 1);
             p = (uint32_t)(ent >> 56);
             const uint64_t r = li / a.n_loc;
-            const uint64_t wid = r * a.n + shard_map(a).vertex(li - r * a.n_loc);
+            const uint64_t wid = r * a.n + a.walks[li];
             wlo = (uint32_t)wid;
             whi = (uint32_t)(wid >> 32);
             pcol[li - base] = p;
@@ -1760,7 +1773,7 @@ __global__ __launch_bounds__(256) void k_rewalk_list(WalkArgs a)
             p = (uint32_t)(e >> 56);
             if (!list_entry_ok(a, li, p)) continue;
             const uint64_t r = li / a.n_loc;
-            const uint64_t wid = r * a.n + shard_map(a).vertex(li - r * a.n_loc);
+            const uint64_t wid = r * a.n + a.walks[li];
             wlo = (uint32_t)wid;
             whi = (uint32_t)(wid >> 32);
             if constexpr (DET) rt = a.rtab + r * L;
@@ -1839,7 +1852,7 @@ __global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* 
                 }
                 pos = p + 1;
                 const uint64_t r = li / a.n_loc;
-                const uint64_t wid = r * a.n + shard_map(a).vertex(li - r * a.n_loc);
+                const uint64_t wid = r * a.n + a.walks[li];
                 wlo = (uint32_t)wid;
                 whi = (uint32_t)(wid >> 32);
                 const uint32_t x = walks[(uint64_t)p * W + li];
@@ -1850,7 +1863,7 @@ __global__ __launch_bounds__(256) void k_rewalk_park(WalkArgs a, const ParkRec* 
                 li = pr.lp & ((1ull << 56) - 1);
                 pos = (uint32_t)(pr.lp >> 56);
                 const uint64_t r = li / a.n_loc;
-                const uint64_t wid = r * a.n + shard_map(a).vertex(li - r * a.n_loc);
+                const uint64_t wid = r * a.n + a.walks[li];
                 wlo = (uint32_t)wid;
                 whi = (uint32_t)(wid >> 32);
                 w.rc = load_rec(a.vrec, pr.cur);
@@ -1993,9 +2006,11 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
                 else hipLaunchKernelGGL((k_rewalk_sorted<M, D>), lgrid, block, 0, s, a);     \
             }                                                                                \
         } else if (rewalk) {                                                                 \
-            hipLaunchKernelGGL((k_rewalk_sweep<M, D>), grid, block, 0, s, a);                \
+            if (a.sh_parts > 1) hipLaunchKernelGGL((k_rewalk_sweep<M, D, true>), grid, block, 0, s, a); \
+            else hipLaunchKernelGGL((k_rewalk_sweep<M, D>), grid, block, 0, s, a);           \
         } else {                                                                             \
-            hipLaunchKernelGGL((k_walk<M, D>), grid, block, 0, s, a);                        \
+            if (a.sh_parts > 1) hipLaunchKernelGGL((k_walk<M, D, true>), grid, block, 0, s, a); \
+            else hipLaunchKernelGGL((k_walk<M, D>), grid, block, 0, s, a);                   \
         }                                                                                    \
     } while (0)
     // a multiple of 8 workgroups: every XCD gets the same number
