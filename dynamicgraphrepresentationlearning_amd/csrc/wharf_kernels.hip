@@ -709,10 +709,7 @@ void launch_anchor_preinit(const WalkArgs& a, const uint64_t* preoff, uint64_t k
 template <bool BLK>
 __device__ __forceinline__ uint32_t start_vertex(const WalkArgs& a, uint64_t j)
 {
-    if constexpr (BLK) {   // 32-bit: set_shard_blocks requires n * wpv < 2^32
-        const uint32_t jj = (uint32_t)j, b = a.sh_bits;
-        return (uint32_t)a.lo + ((((jj >> b) * a.sh_parts + a.sh_part) << b) | (jj & ((1u << b) - 1u)));
-    }
+    if constexpr (BLK) return (uint32_t)shard_map(a).vertex(j);
     return (uint32_t)(a.lo + j);
 }
 
