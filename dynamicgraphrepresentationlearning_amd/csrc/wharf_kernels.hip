@@ -2853,6 +2853,9 @@ __device__ __forceinline__ void patch_slot(uint32_t t, uint64_t e, const uint32_
 #define WHARF_INEDGE_LOADS 4
 #endif
 constexpr uint32_t kInEdgeLoads = WHARF_INEDGE_LOADS;
+#ifndef WHARF_INEDGE_NT
+#define WHARF_INEDGE_NT 1   // A/B: non-temporal pool loads (the pool is read once per batch)
+#endif
 // Round 3: the filter test of the thread's four 16-B loads first, then one
 // wave-uniform branch to the positives (round 2 branched per load: configs[3]
 // pass 2.65-2.73 -> 2.32-2.38 ms with the lean test).  A two-pass form that
@@ -2887,7 +2890,11 @@ __global__ __launch_bounds__(1024, 8) void k_patch_in_edges(const uint32_t* __re
 #pragma unroll
         for (uint32_t u = 0; u < kInEdgeLoads; u++) {
             const uint32_t q = q0 + u * stride;
+#if WHARF_INEDGE_NT
             tv[u] = q < n4 ? __builtin_nontemporal_load(a4 + q) : u32x4{kGap, kGap, kGap, kGap};
+#else
+            tv[u] = q < n4 ? a4[q] : u32x4{kGap, kGap, kGap, kGap};
+#endif
         }
         uint32_t hits = 0;   // 4 bits per load
 #pragma unroll

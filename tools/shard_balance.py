@@ -57,7 +57,7 @@ def main():
         g.generate_initial_random_walks()
         gen = g.stats()
         ids = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device="cuda:0")
-        rec = {k: [] for k in ("ms", "graph", "walk", "steps", "affected", "inits")}
+        rec = {k: [] for k in ("ms", "graph", "walk", "steps", "affected", "inits", "inedge")}
         for b in range(a.batches):
             batch = W.generate_batch_of_edges(5000, n, b, False, False)
             for ins in ((True, False) if a.mixed else (True,)):
@@ -70,12 +70,14 @@ def main():
                 rec["steps"].append(st["steps"])
                 rec["affected"].append(st["affected"])
                 rec["inits"].append(st["last_anchor_inits"])
+                rec["inedge"].append(st["last_csr_move_ms"])
         r = {"shard": i, "shard_def": str(shards[i]), "walks": g.number_of_walks,
              "first_generation_ms": round(first, 2), "generation_ms": round(gen["last_walk_kernel_ms"], 2),
              "generation_steps": gen["steps"], "first_generation_anchor_inits": first_st["last_anchor_inits"],
              "batch_median_ms": round(float(np.median(rec["ms"])), 3),
              "graph_update_median_ms": round(float(np.median(rec["graph"])), 3),
              "walk_update_median_ms": round(float(np.median(rec["walk"])), 3),
+             "in_edge_scan_median_ms": round(float(np.median(rec["inedge"])), 3),
              "rewalk_steps_mean": int(np.mean(rec["steps"])), "affected_mean": int(np.mean(rec["affected"])),
              "anchor_inits_mean": int(np.mean(rec["inits"])), "batch_ms": [round(x, 2) for x in rec["ms"]],
              "rewalk_Gsteps_per_s": round(float(np.sum(rec["steps"]) / np.sum(rec["walk"]) / 1e6), 2),
