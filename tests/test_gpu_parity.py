@@ -203,6 +203,35 @@ def _compare_stream(W, off, adj, batches, wpv=3, L=12, **kw):
     g.destroy()
 
 
+@pytest.mark.parametrize("preinit_all", ["0", "1"])
+@pytest.mark.parametrize("init", [1, 2])   # BURNIN, WEIGHT
+def test_node2vec_anchors_up_front_or_lazily(W, monkeypatch, preinit_all, init):
+    """Every anchor computed at the first generation (round 4's rule: >= 1 walk step
+    per slot) or lazily by the walkers (WHARF_PREINIT_ALL=0): the same corpus,
+    counters, affected ids and CSR as the oracle either way, with few walks per
+    slot (wpv 1, L 20 on ~5 k slots: ~4 steps per slot) and a stream of inserts
+    and deletes, so the re-walks run into states no walker had entered."""
+    monkeypatch.setenv("WHARF_PREINIT_ALL", preinit_all)
+    monkeypatch.setenv("WHARF_NO_PREINIT", "")
+    base = O.generate_batch_of_edges(4000, 1 << 11, 9, False, False)
+    off, adj = O.csr_from_edges(1 << 10, base)
+    batches = [(True, O.generate_batch_of_edges(300, 1 << 10, 21, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
+               (False, O.generate_batch_of_edges(200, 1 << 10, 22, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
+               (True, O.generate_batch_of_edges(300, 1 << 10, 23, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES)]
+    _compare_stream(W, off, adj, batches, wpv=1, L=20, deterministic=False, seed=17, model=1, paramP=0.5,
+                    paramQ=2.0, sampler_init=init)
+    # which path ran: up front, exactly one init per slot (every target has a neighbour: undirected) and
+    # none left for the walkers; lazily, one per state entered, plus duplicates of states two walkers
+    # enter at once (benign: the same value)
+    g = W.WharfMH.from_csr(off, adj, config=W.WharfConfig(walks_per_vertex=1, walk_length=20, deterministic=False,
+                                                          seed=17, model=1, paramP=0.5, paramQ=2.0,
+                                                          sampler_init=init))
+    g.generate_initial_random_walks()
+    inits = g.stats()["last_anchor_inits"]
+    g.destroy()
+    assert (inits == len(adj)) if preinit_all == "1" else (0 < inits != len(adj)), (inits, len(adj))
+
+
 def test_edge_cases_isolated_dead_ends_and_flags(W):
     # vertex 5 isolated, 6 a sink (directed edge 4->6), self loop 3->3
     off = np.array([0, 2, 4, 7, 9, 11, 11, 11], dtype=np.uint64)
