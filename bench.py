@@ -80,6 +80,9 @@ def parse():
     p.add_argument("--cpu-timeout", type=int, default=300)
     p.add_argument("--cpu-length", type=int, default=24,
                    help="walk length of the bounded reference CPU sample (~15-25 s on 16 host threads)")
+    p.add_argument("--cpu-scale", type=int, default=17,
+                   help="RMAT scale of the same-shape CPU baseline (configs[1]'s density, wpv x L of the workload; "
+                        "0 = off)")
     p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     p.add_argument("--n2v-steps", type=int, default=3, help="node2vec warm generations of the mh_node2vec record (0 = off)")
     p.add_argument("--n2v-rewalk-batches", type=int, default=5, help="configs[2] batches of the mh_node2vec record")
@@ -102,6 +105,9 @@ def parse():
                    help="device buffer of the bounded corpus gather (all ranks' rows of one chunk)")
     p.add_argument("--gather-check", type=int, default=1,
                    help="second gather pass checking the checksum of checksums (0 = off)")
+    p.add_argument("--init-dist", action="store_true",
+                   help="initialise torch.distributed even at N = 1 (one rank: runs the RCCL leg -- device "
+                        "collectives, the chunked gather, the 8-GPU jobs -- on a one-GPU box)")
     return p.parse_args()
 
 
@@ -237,6 +243,96 @@ def cpu_baseline(args, n, active_vertices, off, adj, kind):
             "sample": f"oracle/wharf_oracle.c restatement, same graph, walks [0, {w1}), L={args.length}; "
                       f"{steps} steps in {secs:.2f} s", "seconds": secs, "host": host_cpus(),
             "full_workload_steps": full, "full_workload_seconds_extrapolated": round(full / (steps / secs), 1)}
+
+
+def cpu_baseline_same_shape(args, W, torch, dev, extrapolated):
+    """The reference CPU path MEASURED at the workload's walk shape (VERDICT r04
+    missing #2): walks_per_vertex and L of the headline (10 x 80), the
+    headline's model and mode, on an RMAT graph of configs[1]'s density scaled
+    down to --cpu-scale so that generation plus one 10k-edge insert batch fit
+    the time budget; the GPU runs the same graph (same RMAT, bit-exact
+    generator) in the same bench run.  `extrapolated` (the bounded configs[1]
+    sample, linear in steps) is kept as a secondary field."""
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    cores = cpu_cores(args.cpu_threads)
+    S = args.cpu_scale
+    ns = 1 << S
+    samples = args.samples >> max(0, args.scale - S)           # configs[1]'s samples per vertex
+    mode = "deterministic" if args.det else "MH"
+    # the GPU on the same graph: generation (first and warm), the index as the reference builds it
+    # (per-vertex sorted (wid*L+pos, next), here exported to host), one insert batch
+    cfg = W.WharfConfig(walks_per_vertex=args.wpv, walk_length=args.length,
+                        model=W.NODE2VEC if args.model == "node2vec" else W.DEEPWALK, paramP=args.paramP,
+                        paramQ=args.paramQ, deterministic=args.det, seed=0x5EED)
+    g = W.WharfMH.from_rmat(ns, samples, 2 * ns, seed=args.seed, config=cfg, device=dev)
+    m = g.number_of_edges()
+    g.generate_initial_random_walks()
+    g.generate_initial_random_walks()
+    st = g.stats()
+    gsteps, gms = st["steps"], st["last_walk_kernel_ms"]
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    g.generate_initial_random_walks()
+    cnt, keys, nexts = g.inverted_index()
+    gen_idx_ms = (time.perf_counter() - t1) * 1e3
+    del cnt, keys, nexts
+    batch = W.generate_batch_of_edges(5000, ns, 0, False, False, device=dev)
+    out = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    aff = g.insert_edges_batch(batch, remove_dups=True, out=out)
+    torch.cuda.synchronize(dev)
+    gpu_batch_ms = (time.perf_counter() - t1) * 1e3
+    st2 = g.stats()
+    gpu = {"generation_kernel_ms": round(gms, 3), "walk_steps": gsteps,
+           "walk_steps_per_s": round(gsteps / (gms * 1e-3), 1),
+           "generation_plus_index_export_ms": round(gen_idx_ms, 2),
+           "insert_batch_ms": round(gpu_batch_ms, 3), "insert_batch_affected_walks": int(len(aff)),
+           "insert_batch_graph_update_ms": round(st2["last_graph_update_ms"], 3),
+           "insert_batch_walk_update_ms": round(st2["last_walk_update_ms"], 3)}
+    g.destroy()
+    cmd = [harness, "cfg", str(args.wpv), str(args.length), args.model, str(args.paramP), str(args.paramQ), "weight",
+           "1" if args.det else "0", "42", "graph-rmat", str(samples), str(2 * ns), str(args.seed), str(ns),
+           "time-gen", "1", "time-upd", "5000", "0", "0", "1"]
+    log(f"cpu_baseline (same shape): reference harness, {cores} threads: {' '.join(cmd[1:])}")
+    try:
+        r = subprocess.run(cmd, env=dict(os.environ, NUM_THREADS=str(cores)), capture_output=True, text=True,
+                           timeout=args.cpu_timeout)
+    except subprocess.TimeoutExpired:
+        log("cpu_baseline (same shape): harness timed out")
+        return None
+    gen = re.search(r"time-gen seconds=([0-9.]+)", r.stdout)
+    upd = re.search(r"time-upd seconds=([0-9.]+) edges=(\d+) affected=(\d+)", r.stdout)
+    if r.returncode != 0 or not gen:
+        log("cpu_baseline (same shape): harness failed", r.returncode, r.stderr[-500:])
+        return None
+    secs = float(gen.group(1))
+    steps = gsteps   # the same graph, start vertices and walk shape: the transitions both paths append
+    rec = {"value": round(steps / secs, 1), "unit": "walk-steps/s", "cores": cores, "kind": "reference",
+           "sample": f"reference WharfMH::generate_initial_random_walks MEASURED at the workload's walk shape "
+                     f"(walks_per_vertex={args.wpv}, L={args.length}, {mode} {args.model}) on RMAT scale {S} "
+                     f"(n={ns}, {samples} undirected samples = configs[1]'s per-vertex density, m={m}); "
+                     f"{steps} transitions in {secs:.2f} s",
+           "seconds": secs, "graph": {"scale": S, "n": ns, "m": m, "samples": samples, "seed": args.seed},
+           "host": host_cpus(),
+           "gpu_same_graph": gpu,
+           "gpu_over_cpu_generation": round(gpu["walk_steps_per_s"] / (steps / secs), 1),
+           "index_build_asymmetry": "the reference's timed generate also builds its per-vertex inverted index "
+                                    "(wharfmh.h:329-354); the GPU's walk_steps_per_s is the walk kernel alone, its "
+                                    "index is a derived export: gpu_same_graph.generation_plus_index_export_ms "
+                                    "times generation + the full index sorted on the device and copied to host",
+           "gpu_over_cpu_generation_with_index": round(secs * 1e3 / gen_idx_ms, 1)}
+    if upd:
+        rec["insert_batch"] = {"cpu_ms": round(float(upd.group(1)) * 1e3, 1), "edges": int(upd.group(2)),
+                               "cpu_affected_walks": int(upd.group(3)), "gpu_ms": gpu["insert_batch_ms"],
+                               "gpu_over_cpu": round(float(upd.group(1)) * 1e3 / gpu_batch_ms, 1),
+                               "batch": "generate_batch_of_edges(5000, n, 0, false, undirected), remove_dups, "
+                                        "walk update applied (memory-throughput-latency.cpp:126-134)"}
+    if extrapolated:
+        rec["configs1_extrapolation"] = extrapolated
+    return rec
 
 
 def cpu_baseline_deterministic(args, batches=3):
@@ -712,7 +808,7 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
                "generation_walk_steps_per_s": round(gsum[0] / (gmax[1] * 1e-3), 1),
                "first_generation_anchor_inits": int(gsum[1]),
                "device_bytes_rank0": g.memory_footprint(verbose=False)["total_bytes"]}
-        if args.job_gather and world > 1:
+        if args.job_gather and dist:
             free = torch.cuda.mem_get_info(dev)[0] if comm_dev != "cpu" else (8 << 30)
             budget = max(64 << 20, min(args.gather_chunk_bytes, free // 4))
             rec["corpus_allgatherv"] = corpus_gather_record(args, torch, dist, g, shards[:world], n, 10, 80, dev,
@@ -812,7 +908,7 @@ def main():
     dev = local % max(torch.cuda.device_count(), 1)
     backend = os.environ.get("WHARF_DIST_BACKEND", "nccl")   # gloo: rehearsal of the N>1 path on one GPU
     comm_dev = "cpu" if backend == "gloo" else f"cuda:{dev}"
-    if world > 1:
+    if world > 1 or args.init_dist:
         import torch.distributed as dist
         torch.cuda.set_device(dev)
         if backend == "nccl":
@@ -906,7 +1002,7 @@ def main():
 
     # BASELINE's two 8-GPU jobs on the ranks of this run (configs[3] strong, configs[4] g-of-8 weak)
     jobs = None
-    if world > 1 and args.jobs and args.model == "deepwalk" and not args.det:
+    if (world > 1 or dist) and args.jobs and args.model == "deepwalk" and not args.det:
         jobs = {}
         for name in [j for j in args.jobs.split(",") if j]:
             torch.cuda.empty_cache()
@@ -964,11 +1060,19 @@ def main():
             "rewalk_latency_10k_batch_deterministic": rewalk_det,
             "streaming_rooflines": streaming_rooflines(rewalk, rewalk_det, args.scale),
             "corpus_allgatherv": corpus,
+            "dist_backend": (backend if backend == "gloo" else "nccl (RCCL)") if dist else None,
             "cpu_baseline": None,
         }
         if world == 1 and args.cpu_baseline != "off":
             active = int((deg > 0).sum())
-            line["cpu_baseline"] = cpu_baseline(args, n, active, off, adj, args.cpu_baseline)
+            ext = cpu_baseline(args, n, active, off, adj, args.cpu_baseline)
+            same = None
+            if args.cpu_baseline in ("auto", "reference") and args.cpu_scale > 0:
+                try:
+                    same = cpu_baseline_same_shape(args, W, torch, dev, ext)
+                except Exception as ex:   # noqa: BLE001 (the extrapolated sample stays the baseline)
+                    log(f"cpu_baseline (same shape) failed: {ex}")
+            line["cpu_baseline"] = same or ext
             if args.cpu_baseline in ("auto", "reference") and args.det_rewalk_batches > 0:
                 line["cpu_baseline_deterministic"] = cpu_baseline_deterministic(args)
         print(json.dumps(line), flush=True)

@@ -1246,7 +1246,7 @@ void wharf_config_default(wharf_config* c)
     std::memset(c, 0, sizeof(*c));
     c->walks_per_vertex = 10;              // globals.h:7
     c->walk_length = 80;                   // globals.h:10
-    c->model = WHARF_DEEPWALK;             // experiments' default (-model deepwalk, throughput-latency.cpp:13)
+    c->model = WHARF_NODE2VEC;             // globals.h:13 (the experiments pass -model deepwalk explicitly)
     c->paramP = 4.0f;                      // globals.h:16
     c->paramQ = 1.0f;                      // globals.h:19
     c->sampler_init = WHARF_INIT_WEIGHT;   // globals.h:22

@@ -45,7 +45,7 @@ class WharfConfig:
 
     walks_per_vertex: int = 10
     walk_length: int = 80
-    model: int = DEEPWALK
+    model: int = NODE2VEC          # globals.h:13 (in deterministic mode both models give the same walks)
     paramP: float = 4.0
     paramQ: float = 1.0
     sampler_init: int = WEIGHT

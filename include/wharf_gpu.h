@@ -55,7 +55,7 @@ enum { WHARF_SORTED = 1, WHARF_REMOVE_DUPS = 2, WHARF_APPLY_WALK_UPDATES = 4,
 typedef struct wharf_config {
     uint32_t walks_per_vertex;  /* config::walks_per_vertex (u8 in the reference), default 10 */
     uint32_t walk_length;       /* config::walk_length (u8), default 80, 2..255 */
-    int32_t  model;             /* config::random_walk_model, default WHARF_DEEPWALK */
+    int32_t  model;             /* config::random_walk_model, default WHARF_NODE2VEC (globals.h:13) */
     float    paramP;            /* config::paramP, default 4.0 */
     float    paramQ;            /* config::paramQ, default 1.0 */
     int32_t  sampler_init;      /* config::sampler_init_strategy, default WHARF_INIT_WEIGHT */

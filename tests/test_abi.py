@@ -80,6 +80,7 @@ def test_config_defaults_mirror_reference_globals():
     # config/globals.h:7-29
     assert (c.walks_per_vertex, c.walk_length, c.sampler_init, c.deterministic) == (10, 80, 2, 1)
     assert (c.paramP, c.paramQ) == (4.0, 1.0)
+    assert c.model == L.WHARF_NODE2VEC            # config::random_walk_model = NODE2VEC (globals.h:13)
 
 
 def test_errors_without_a_device_are_reported_not_crashed():

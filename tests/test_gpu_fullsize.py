@@ -79,7 +79,7 @@ def _all_edges(torch, ekeys, n, u, v):
 def test_configs1_full_size_generation(W, torch):
     n = 1 << 22
     sent = int(np.uint32(W.SENTINEL).view(np.int32))
-    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=L, deterministic=False, seed=0x5EED)
+    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=L, model=W.DEEPWALK, deterministic=False, seed=0x5EED)
     g = W.WharfMH.from_rmat(n, 117_185_083, 2 * n, seed=2, config=cfg)
     off, adj = g.flatten_graph()
     ekeys, deg = _edge_keys(torch, off, adj, n)
@@ -94,7 +94,7 @@ def test_configs1_full_size_generation(W, torch):
     for p in (0, 1, 2, 39, 78):
         assert _all_edges(torch, ekeys, n, w[p, ~iso], w[p + 1, ~iso]), f"non-edge transition at {p}"
     w0 = 31_000_000
-    ref = O.Engine(off, adj, wpv=10, L=L, deterministic=False, seed=0x5EED)
+    ref = O.Engine(off, adj, wpv=10, L=L, model=O.DEEPWALK, deterministic=False, seed=0x5EED)
     ref.time_generate_range(w0, w0 + 4096)
     mine = w[:, w0:w0 + 4096].T.contiguous().cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(mine, ref.walks_range(w0, w0 + 4096))
@@ -104,7 +104,7 @@ def test_configs1_full_size_generation(W, torch):
 def test_configs2_full_size_insert_batch(W, torch):
     n = 1 << 22
     sent = int(np.uint32(W.SENTINEL).view(np.int32))
-    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=L, deterministic=False, seed=0x5EED)
+    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=L, model=W.DEEPWALK, deterministic=False, seed=0x5EED)
     g = W.WharfMH.from_rmat(n, 43_000_000, 2 * n, seed=3, config=cfg)
     g.generate_initial_random_walks()
     before = _dev_walks(torch, g)
@@ -221,7 +221,7 @@ def test_index_keys_past_2_32(W, torch):
     vertex, 64-bit keys above 2^32 present and equal to wid*L + pos of a walk
     that holds the vertex there, next = the following position."""
     n, wpv, Lk = 1 << 20, 255, 17
-    cfg = W.WharfConfig(walks_per_vertex=wpv, walk_length=Lk, deterministic=False, seed=11)
+    cfg = W.WharfConfig(walks_per_vertex=wpv, walk_length=Lk, model=W.DEEPWALK, deterministic=False, seed=11)
     g = W.WharfMH.from_rmat(n, 8_000_000, 2 * n, seed=4, config=cfg)
     g.generate_initial_random_walks()
     Wn = g.number_of_walks
@@ -271,7 +271,7 @@ def test_configs3_full_size_shard_of_8(W, torch):
     from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards
     n = 1 << 25
     sent = int(np.uint32(W.SENTINEL).view(np.int32))
-    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=L, deterministic=False, seed=0x5EED)
+    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=L, model=W.DEEPWALK, deterministic=False, seed=0x5EED)
     g = W.WharfMH.from_rmat(n, 1_200_000_000, 2 * n, seed=4, config=cfg)
     off, adj = g.flatten_graph()
     deg_h = np.diff(off.astype(np.int64))
@@ -292,7 +292,7 @@ def test_configs3_full_size_shard_of_8(W, torch):
     for p in (0, 1, 39, 78):
         assert _all_edges(torch, ekeys, n, before[p, ~iso], before[p + 1, ~iso]), f"non-edge transition at {p}"
     # oracle window: round 0, the shard's first 4096 start vertices (= local columns 0..4095)
-    ref = O.Engine(off, adj, wpv=10, L=L, deterministic=False, seed=0x5EED)
+    ref = O.Engine(off, adj, wpv=10, L=L, model=O.DEEPWALK, deterministic=False, seed=0x5EED)
     ref.time_generate_range(lo, lo + 4096)
     mine = before[:, :4096].T.contiguous().cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(mine, ref.walks_range(lo, lo + 4096))

@@ -360,10 +360,10 @@ def test_affected_ids_on_device_match_host_list(W):
     import torch
     base = O.generate_batch_of_edges(60000, 1 << 13, 9, False, False)
     off, adj = O.csr_from_edges(1 << 13, base)
-    cfg = W.WharfConfig(walks_per_vertex=3, walk_length=30, deterministic=False, seed=7)
+    cfg = W.WharfConfig(walks_per_vertex=3, walk_length=30, model=W.DEEPWALK, deterministic=False, seed=7)
     gh = W.WharfMH.from_csr(off, adj, config=cfg)
     gd = W.WharfMH.from_csr(off, adj, config=cfg)
-    ref = O.Engine(off, adj, wpv=3, L=30, deterministic=False, seed=7)
+    ref = O.Engine(off, adj, wpv=3, L=30, model=O.DEEPWALK, deterministic=False, seed=7)
     gh.generate_initial_random_walks()
     gd.generate_initial_random_walks()
     ref.generate()
@@ -584,7 +584,7 @@ def test_walk_readout_snapshot_follows_every_change(W, monkeypatch):
     (WHARF_WALK_NO_SNAPSHOT=1), text included."""
     base = O.generate_batch_of_edges(60000, 1 << 17, 4, False, False)
     off, adj = O.csr_from_edges(1 << 16, base)          # 2 snapshot chunks per round: several chunks in play
-    cfg = W.WharfConfig(walks_per_vertex=2, walk_length=12, deterministic=False, seed=3)
+    cfg = W.WharfConfig(walks_per_vertex=2, walk_length=12, model=W.DEEPWALK, deterministic=False, seed=3)
     g = W.WharfMH.from_csr(off, adj, config=cfg)
     rng = np.random.default_rng(5)
 
@@ -709,10 +709,10 @@ def test_mh_node2vec_bit_exact_vs_oracle(W, init, pq):
 def test_mh_deepwalk_bit_exact_and_uniform(W):
     z = np.load(os.path.join(G, "wiki_csr.npz"))
     off, adj = z["off"], z["adj"]
-    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, deterministic=False, seed=42)
+    cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, model=W.DEEPWALK, deterministic=False, seed=42)
     g = W.WharfMH.from_csr(off, adj, config=cfg)
     g.generate_initial_random_walks()
-    ref = O.Engine(off, adj, wpv=10, L=80, deterministic=False, seed=42)
+    ref = O.Engine(off, adj, wpv=10, L=80, model=O.DEEPWALK, deterministic=False, seed=42)
     ref.generate()
     w = g.walks()
     np.testing.assert_array_equal(w, ref.walks())
@@ -828,7 +828,7 @@ def test_large_rmat_properties(W):
     wid % n, isolated starts stay length 1, steps = active walks * (L-1);
     a sample of walks is re-computed by the oracle bit for bit."""
     n = 1 << 20
-    cfg = W.WharfConfig(walks_per_vertex=4, walk_length=80, deterministic=False, seed=7)
+    cfg = W.WharfConfig(walks_per_vertex=4, walk_length=80, model=W.DEEPWALK, deterministic=False, seed=7)
     g = W.WharfMH.from_rmat(n, 8_000_000, 2 * n, seed=2, config=cfg)
     off, adj = g.flatten_graph()
     deg = np.diff(off.astype(np.int64))
@@ -847,7 +847,7 @@ def test_large_rmat_properties(W):
         cols = rng.choice(np.nonzero(~iso)[0], 20000, replace=False)
         u, v = w[p, cols].astype(np.int64), w[p + 1, cols].astype(np.int64)
         assert _has_edge(off, adj, u, v).all()
-    ref = O.Engine(off, adj, wpv=4, L=80, deterministic=False, seed=7)
+    ref = O.Engine(off, adj, wpv=4, L=80, model=O.DEEPWALK, deterministic=False, seed=7)
     ref.time_generate_range(123456, 123456 + 4096)
     rw = ref.walks()[123456:123456 + 4096]
     np.testing.assert_array_equal(w[:, 123456:123456 + 4096].T, rw)
