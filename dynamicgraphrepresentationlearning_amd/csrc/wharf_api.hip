@@ -124,7 +124,9 @@ struct wharf_handle {
     DevBuf stab;                               // node2vec MH re-walk: start-state anchor table (k_rewalk_sorted)
     DevBuf sanc;                               // anchor carry: the sources' old anchor entries (k_save_rows)
     DevBuf rchunk;                             // per batch source: chunk counts, then their exclusive prefix (k_*_rows_c)
-    bool symmetric = false;                    // every edge's reverse is an edge (anchor carry needs it)
+    bool symmetric = false;                    // every edge's reverse is an edge (anchor carry and rev need it)
+    DevBuf rev, srev;                          // reverse-slot index (k_patch_rev) and the sources' old entries
+    bool rev_on = false, rev_valid = false;    // the index is kept / matches the pool (a repack invalidates it)
     DevBuf park, parkc;                        // node2vec MH re-walk passes: two parked-walker lists, their counts
     DevBuf bdesc;                              // node2vec MH block re-walk: per 256-walk block, its run of the list
     uint32_t st_park_passes = 0;               // passes of the last re-walk by passes (0: lock-step kernel)
@@ -446,6 +448,7 @@ struct wharf_handle {
         launch_vrec(off.as<uint64_t>(), deg.as<uint32_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
         launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rs, 1, s);
         repacks++;
+        rev_valid = false;   // every row moved: the reverse-slot index is rebuilt after the batch
     }
 
     // In-place compaction (k_compact_gather / k_compact_put): rows in slot
@@ -512,6 +515,7 @@ struct wharf_handle {
         launch_vrec(off.as<uint64_t>(), deg.as<uint32_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
         launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rs, 1, s);
         repacks++;
+        rev_valid = false;   // every row moved: the reverse-slot index is rebuilt after the batch
     }
 
     void scan_u64(uint64_t* in, uint64_t* out, uint64_t cnt)
@@ -530,6 +534,42 @@ struct wharf_handle {
         if (anchors) build_filters();
         bitmap.ensure((bitmap_words() + kFilterWords) * 4);   // exact bitmap, then the Bloom filter
         sync();
+        rev_on = symmetric && rev_wanted();
+        if (rev_on) build_rev();
+    }
+
+    // The reverse-slot index (k_patch_rev) on undirected graphs, unless WHARF_REV=0; by
+    // default only when its 8 B per pool slot leave room for the walk matrix of every walk
+    // the handle may own and a margin (configs[3]: 21 GB next to a 56 GB graph and 107 GB of
+    // walks; configs[4]'s 33 GB do not fit beside its 226 GB graph: it keeps the scan)
+    bool rev_wanted() const
+    {
+        const char* e = getenv("WHARF_REV");
+        if (e && *e) return atoi(e) != 0;
+        const uint64_t walks_all = (uint64_t)n * wpv * L * 4, margin = 16ull << 30;
+        return std::max<uint64_t>(pool_cap, 1) * 8 + walks_all + margin <= free_bytes();
+    }
+
+    void build_rev()
+    {
+        rev.ensure(std::max<uint64_t>(pool_cap, 1) * 8);
+        HIPCHK(hipMemsetAsync(rev.p, 0xFF, std::max<uint64_t>(pool_cap, 1) * 8, s));   // kNoRev
+        unsigned long long* miss = errflag.as<unsigned long long>() + 4;
+        HIPCHK(hipMemsetAsync(miss, 0, 8, s));
+        launch_rev_build(off.as<uint64_t>(), deg.as<uint32_t>(), adj.as<uint32_t>(), n, pool_used, rev.as<uint64_t>(),
+                         miss, s);
+        unsigned long long v = 0;
+        HIPCHK(hipMemcpyAsync(&v, miss, 8, hipMemcpyDeviceToHost, s));
+        sync();
+        rev_valid = v == 0;
+        if (!rev_valid) drop_rev();   // not symmetric after all: the scan keeps the records
+    }
+
+    void drop_rev()
+    {
+        rev_on = rev_valid = false;
+        rev.release();
+        srev.release();
     }
 
     // the walk matrix is allocated on first use (and re-allocated by set_shard)
@@ -773,7 +813,8 @@ void free_handle(wharf_handle* h)
                       &h->fplan, &h->memo, &h->srcidx, &h->row_epoch, &h->off2, &h->adj2, &h->walks, &h->aff, &h->rtab,
                       &h->bitmap, &h->counters, &h->errflag, &h->tmp, &h->k1, &h->k2, &h->flags, &h->chg, &h->cf,
                       &h->runstart, &h->runs, &h->count, &h->pairs, &h->sel, &h->defer, &h->rplan, &h->pscan,
-                      &h->scratch, &h->stab, &h->preoff, &h->park, &h->parkc, &h->bdesc, &h->sanc, &h->rchunk})
+                      &h->scratch, &h->stab, &h->preoff, &h->park, &h->parkc, &h->bdesc, &h->sanc, &h->rchunk,
+                      &h->rev, &h->srev})
         b->release();
     h->free_snaps();
     for (auto& e : h->ev)
@@ -787,7 +828,7 @@ void build_graph_from_keys(wharf_handle* h, uint64_t cnt, bool drop_loops, bool 
 {
     const uint64_t mm = h->unique_keys(cnt, drop_loops, 32 + std::max<uint32_t>(bits_for(h->n), 1));
     h->symmetric = symmetric_by_construction;
-    if (!symmetric_by_construction && h->anchors) {   // (only node2vec MH's anchor carry asks)
+    if (!symmetric_by_construction && (h->anchors || h->rev_wanted())) {   // (the anchor carry and rev ask)
         unsigned long long* asym = h->errflag.as<unsigned long long>() + 3;
         HIPCHK(hipMemsetAsync(asym, 0, 8, h->s));
         launch_keys_symmetric(h->k1.as<uint64_t>(), mm, asym, h->s);
@@ -1112,7 +1153,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         unsigned long long batch_asym = 0;
         HIPCHK(hipMemcpyAsync(&k, h->count.p, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(&total_chg, h->cf.as<uint32_t>() + mb, 4, hipMemcpyDeviceToHost, s));
-        if (h->anchors && h->symmetric) {   // a batch without every reverse edge leaves the graph directed
+        if ((h->anchors || h->rev_on) && h->symmetric) {   // a batch without every reverse edge leaves the graph directed
             unsigned long long* asym = h->errflag.as<unsigned long long>() + 3;
             HIPCHK(hipMemsetAsync(asym, 0, 8, s));
             launch_keys_symmetric(bkeys, mb, asym, s);
@@ -1170,6 +1211,11 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->epoch = epoch;
         h->dead_slots += dead;
         if (batch_asym) h->symmetric = false;
+        if (h->rev_on && !h->symmetric) h->drop_rev();
+        // reverse-slot index: carried through the merge and used for the in-edge records
+        // unless a repack or compaction of this batch moved every row (then: scan, rebuild)
+        const bool use_rev = h->rev_on && h->rev_valid;
+        if (use_rev) h->srev.ensure_grow(std::max<uint64_t>(saved, 1) * 8);
         // Anchor carry (node2vec MH on an undirected graph): the entries of the sources' rows travel
         // through the merge and only those whose anchor can change are reset (k_anchor_invalidate);
         // otherwise every entry of a rebuilt row starts empty.  WHARF_ANCHOR_CARRY=0 (A/B, tests).
@@ -1190,10 +1236,12 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             return rocprim::exclusive_scan(t, b, rcnt, rpre, 0u, (size_t)(k + 1), rocprim::plus<uint32_t>(), s);
         });
         launch_save_rows(h->runs.as<RunInfo>(), k, rpre, h->adj.as<uint32_t>(), sofs, h->scratch.as<uint32_t>(), anc_base,
-                         carry ? h->sanc.as<uint64_t>() : nullptr, s);
+                         carry ? h->sanc.as<uint64_t>() : nullptr, use_rev ? h->rev.as<uint64_t>() : nullptr,
+                         use_rev ? h->srev.as<uint64_t>() : nullptr, s);
         launch_merge_rows(h->runs.as<RunInfo>(), k, rpre, bkeys, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(),
                           h->scratch.as<uint32_t>(), sofs, relofs, h->pool_used, insert, h->rplan.as<RowPlan>(),
-                          h->adj.as<uint32_t>(), carry ? h->sanc.as<uint64_t>() : nullptr, anc_base, s);
+                          h->adj.as<uint32_t>(), carry ? h->sanc.as<uint64_t>() : nullptr, anc_base,
+                          use_rev ? h->srev.as<uint64_t>() : nullptr, use_rev ? h->rev.as<uint64_t>() : nullptr, s);
         launch_commit_rows(h->runs.as<RunInfo>(), k, h->rplan.as<RowPlan>(), h->epoch, h->off.as<uint64_t>(),
                            h->deg.as<uint32_t>(), h->cap.as<uint32_t>(), h->vrec.as<ERec>(), h->row_epoch.as<uint32_t>(), s);
         h->pool_used += grow;
@@ -1203,9 +1251,27 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         launch_erec_rows(h->runs.as<RunInfo>(), k, rpre, h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->adj.as<uint32_t>(),
                          h->vrec.as<ERec>(), h->erec.as<ERec>(), rs, carry ? 1 : 0, s);
         HIPCHK(hipEventRecord(h->ev[4], s));
-        launch_patch_in_edges(h->adj.as<uint32_t>(), h->pool_used, h->bitmap.as<uint32_t>(),
-                              h->bitmap.as<uint32_t>() + h->bitmap_words(), h->vrec.as<ERec>(), h->erec.as<ERec>(), rs, s);
+        bool scan = !use_rev;
+        if (use_rev) {   // the sources' in-edges from their own rows (k_patch_rev)
+            unsigned long long* miss = h->errflag.as<unsigned long long>() + 4;
+            HIPCHK(hipMemsetAsync(miss, 0, 8, s));
+            launch_patch_rev(h->runs.as<RunInfo>(), k, rpre, h->off.as<uint64_t>(), h->deg.as<uint32_t>(),
+                             h->adj.as<uint32_t>(), h->bitmap.as<uint32_t>(), h->vrec.as<ERec>(), h->erec.as<ERec>(), rs,
+                             h->rev.as<uint64_t>(), miss, s);
+            unsigned long long v = 0;
+            HIPCHK(hipMemcpyAsync(&v, miss, 8, hipMemcpyDeviceToHost, s));
+            h->sync();
+            if (v) {   // an edge without its reverse: cannot happen on a graph tracked as symmetric
+                h->drop_rev();
+                scan = true;
+            }
+        }
+        if (scan)
+            launch_patch_in_edges(h->adj.as<uint32_t>(), h->pool_used, h->bitmap.as<uint32_t>(),
+                                  h->bitmap.as<uint32_t>() + h->bitmap_words(), h->vrec.as<ERec>(), h->erec.as<ERec>(),
+                                  rs, s);
         HIPCHK(hipEventRecord(h->ev[5], s));
+        if (h->rev_on && !h->rev_valid) h->build_rev();   // after a repack / compaction in this batch
         h->st.last_moved_slots = h->pool_used;
         if (h->anchors) {
             // the edge set changes by the batch's changing edges only; rebuild when
@@ -1915,7 +1981,7 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     wharf_memory r{};
     r.n = h->n;
     r.m = h->m;
-    r.csr_bytes = h->off.cap + h->adj.cap + h->deg.cap + h->cap.cap;
+    r.csr_bytes = h->off.cap + h->adj.cap + h->deg.cap + h->cap.cap + h->rev.cap;
     r.records_bytes = h->vrec.cap + h->erec.cap;
     r.walks_bytes = h->walks.cap + h->aff.cap;
     const uint64_t anchor_part = h->anchors ? h->erec.cap / 2 : 0;   // bytes 16-31 of the 32-B records
@@ -1923,7 +1989,7 @@ int wharf_memory_footprint(const wharf_handle* h, wharf_memory* out)
     r.samplers_bytes = anchor_part + h->row_epoch.cap;
     r.edge_hash_bytes = h->ehash.cap + h->fdir.cap + h->fpool.cap;
     r.update_buffers_bytes = h->off2.cap + h->adj2.cap + h->erec2.cap + h->scratch.cap + h->rplan.cap + h->pscan.cap +
-                             h->sanc.cap;   // the anchor carry's saved entries (8 B per saved slot)
+                             h->sanc.cap + h->srev.cap;   // the anchor carry's / reverse index's saved entries
     r.scratch_bytes = h->tmp.cap + h->k1.cap + h->k2.cap + h->flags.cap + h->chg.cap + h->cf.cap + h->runstart.cap +
                       h->runs.cap + h->fplan.cap + h->memo.cap + h->srcidx.cap + h->count.cap + h->pairs.cap +
                       h->sel.cap + h->defer.cap + h->park.cap + h->parkc.cap + h->stab.cap + h->preoff.cap + h->rtab.cap + h->bitmap.cap + h->counters.cap +

@@ -1647,7 +1647,11 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
             // buffer written in whole rows plus a merge pass that rewrites the
             // matrix rows whole cost as much (sorted 57 -> 47 ms, merge 9.8 ms;
             // profiles/r02/n2v_rewalk2)
+#ifndef WHARF_PROBE_NO_REWALK_STORE   // timing probe only (tools/ab_build.sh): the walks are not written
             if (active && pos > p) __builtin_nontemporal_store(val, walks + (uint64_t)pos * W + li);
+#else
+            steps += val == 0xFFFFFFFDu;   // keeps val live; never true for a vertex id < 2^32 - 2
+#endif
         }
     }
     wave_add(a.counters + 0, steps);
@@ -2470,13 +2474,15 @@ __global__ void k_plan_rows(const RunInfo* __restrict__ runs, uint64_t k, const 
 // with sanc, its anchor entries too (anchor carry, k_anchor_invalidate)
 __global__ void k_save_rows(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ adj,
                             const uint64_t* __restrict__ sofs, uint32_t* __restrict__ scratch,
-                            const uint64_t* __restrict__ anc, uint64_t* __restrict__ sanc)
+                            const uint64_t* __restrict__ anc, uint64_t* __restrict__ sanc,
+                            const uint64_t* __restrict__ rev, uint64_t* __restrict__ srev)
 {
     const RunInfo ri = runs[blockIdx.x];
     uint32_t* __restrict__ out = scratch + sofs[blockIdx.x];
     for (uint64_t i = threadIdx.x; i < ri.end - ri.off; i += blockDim.x) {
         out[i] = adj[ri.off + i];
         if (sanc) sanc[sofs[blockIdx.x] + i] = anc[(ri.off + i) * kAnchorStride];
+        if (srev) srev[sofs[blockIdx.x] + i] = rev[ri.off + i];
     }
 }
 
@@ -2512,7 +2518,8 @@ __global__ void k_merge_rows(const RunInfo* __restrict__ runs, const uint64_t* _
                              const uint32_t* __restrict__ scratch, const uint64_t* __restrict__ sofs,
                              const uint64_t* __restrict__ relofs, uint64_t pool_end, int insert,
                              RowPlan* __restrict__ plan, uint32_t* __restrict__ adj,
-                             const uint64_t* __restrict__ sanc, uint64_t* __restrict__ anc)
+                             const uint64_t* __restrict__ sanc, uint64_t* __restrict__ anc,
+                             const uint64_t* __restrict__ srev, uint64_t* __restrict__ rev)
 {
     const uint64_t j = blockIdx.x;
     const RunInfo ri = runs[j];
@@ -2532,6 +2539,7 @@ __global__ void k_merge_rows(const RunInfo* __restrict__ runs, const uint64_t* _
         if (at != ~0ull) {
             adj[at] = x;
             if (sanc) anc[at * kAnchorStride] = sanc[sofs[j] + i];   // the entry travels with its edge
+            if (srev) rev[at] = srev[sofs[j] + i];
         }
     }
     if (insert) {
@@ -2541,6 +2549,7 @@ __global__ void k_merge_rows(const RunInfo* __restrict__ runs, const uint64_t* _
             const uint64_t at = noff + (cf[ri.rs + t] - base) + lower_bound_u32(old, d, x);
             adj[at] = x;
             if (sanc) anc[at * kAnchorStride] = kAnchorNone64;
+            if (srev) rev[at] = kNoRev;
         }
     }
     if (reloc) {
@@ -2600,7 +2609,8 @@ __device__ __forceinline__ bool run_chunk(const uint32_t* __restrict__ pre, uint
 
 __global__ void k_save_rows_c(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
                               const uint32_t* __restrict__ adj, const uint64_t* __restrict__ sofs,
-                              uint32_t* __restrict__ scratch, const uint64_t* __restrict__ anc, uint64_t* __restrict__ sanc)
+                              uint32_t* __restrict__ scratch, const uint64_t* __restrict__ anc, uint64_t* __restrict__ sanc,
+                              const uint64_t* __restrict__ rev, uint64_t* __restrict__ srev)
 {
     for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
         uint64_t j;
@@ -2613,6 +2623,7 @@ __global__ void k_save_rows_c(const RunInfo* __restrict__ runs, const uint32_t* 
         for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
             out[i] = adj[ri.off + i];
             if (sanc) sanc[sofs[j] + i] = anc[(ri.off + i) * kAnchorStride];
+            if (srev) srev[sofs[j] + i] = rev[ri.off + i];
         }
     }
 }
@@ -2622,7 +2633,8 @@ __global__ void k_merge_rows_c(const RunInfo* __restrict__ runs, const uint32_t*
                                const uint32_t* __restrict__ cf, const uint32_t* __restrict__ scratch,
                                const uint64_t* __restrict__ sofs, const uint64_t* __restrict__ relofs, uint64_t pool_end,
                                int insert, const RowPlan* __restrict__ plan, uint32_t* __restrict__ adj,
-                               const uint64_t* __restrict__ sanc, uint64_t* __restrict__ anc)
+                               const uint64_t* __restrict__ sanc, uint64_t* __restrict__ anc,
+                               const uint64_t* __restrict__ srev, uint64_t* __restrict__ rev)
 {
     for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
         uint64_t j;
@@ -2647,6 +2659,7 @@ __global__ void k_merge_rows_c(const RunInfo* __restrict__ runs, const uint32_t*
             if (at != ~0ull) {
                 adj[at] = x;
                 if (sanc) anc[at * kAnchorStride] = sanc[sofs[j] + i];   // the entry travels with its edge
+                if (srev) rev[at] = srev[sofs[j] + i];
             }
         }
         if (insert && c == 0) {
@@ -2656,6 +2669,7 @@ __global__ void k_merge_rows_c(const RunInfo* __restrict__ runs, const uint32_t*
                 const uint64_t at = noff + (cf[ri.rs + e] - base) + lower_bound_u32(old, d, x);
                 adj[at] = x;
                 if (sanc) anc[at * kAnchorStride] = kAnchorNone64;
+                if (srev) rev[at] = kNoRev;
             }
         }
         if (reloc) {
@@ -2913,6 +2927,106 @@ __global__ __launch_bounds__(1024, 8) void k_patch_in_edges(const uint32_t* __re
         const uint32_t x = adj[e];
         if (bloom_test_big(s_bloom, x)) patch_slot(x, e, bitmap, vrec, erec, rs);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Reverse-slot index (round 5; the survey's optional rev[e]).  On
+// an undirected graph the in-edges of a batch source s are the reverses of its
+// out-edges: the slot of (y -> s) in y's row, for y in N(s).  rev[e] (u64, one
+// per pool slot) holds, for slot e = (x -> y), the slot of (y -> x).  With it
+// the records of the sources' in-edges are patched from the sources' own rows —
+// Σ deg(s) direct record writes — instead of the streaming scan of every pool
+// slot (k_patch_in_edges, 4 B per slot: 10.9 GB per batch at configs[3]).  Kept
+// valid through a batch:
+//  * the entries of the sources' rows travel through k_save_rows / k_merge_rows
+//    with their edges (a new edge starts kNoRev);
+//  * k_patch_rev recomputes an entry whose target is itself a batch source (its
+//    row was rebuilt) or new, by a search of s in the target's new row, and
+//    writes the reverse slot's entry with its record (rev[r] = q);
+//  * a repack or compaction moves every row: the index is rebuilt from scratch
+//    (k_rev_owner + k_rev_build, one search per slot), as at creation.
+// Directed graphs (or batches) keep the scan.  Same records either way, so no
+// result changes (the parity suite runs both: WHARF_REV=0 / 1).
+// ---------------------------------------------------------------------------
+// pass 1 of a build: rev[e] = the owner row of slot e (one wave per row; slack slots stay kNoRev)
+__global__ void k_rev_owner(const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg, uint64_t n,
+                            uint64_t* __restrict__ rev)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t v = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); v < n; v += waves) {
+        const uint64_t o = off[v];
+        const uint32_t d = deg[v];
+        for (uint32_t i = lane; i < d; i += 64) rev[o + i] = v;
+    }
+}
+
+// pass 2, in place: owner x of slot e = (x -> y) -> the slot of (y -> x) (a search of x in y's row)
+__global__ void k_rev_build(const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg,
+                            const uint32_t* __restrict__ adj, uint64_t slots, uint64_t* __restrict__ rev,
+                            unsigned long long* __restrict__ miss)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < slots; e += stride) {
+        const uint64_t x = rev[e];
+        if (x == kNoRev) continue;
+        const uint32_t y = adj[e];
+        const int64_t r = row_find(adj, Row{y, deg[y], 0u, off[y]}, (uint32_t)x);
+        if (r < 0) *miss = 1ull;   // (a plain store: every writer writes 1) the graph is not symmetric
+        rev[e] = r < 0 ? kNoRev : (uint64_t)r;
+    }
+}
+
+// Per batch, after the sources' rows and records are committed (k_commit_rows,
+// k_erec_rows): slot q = (s -> y) of source s's new row gives its reverse r, whose
+// record becomes s's new row and whose entry points back at q.  Chunks of the
+// sources' rows dealt as in k_erec_rows_c (a hub source's row spreads over the chip).
+__global__ void k_patch_rev(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
+                            const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg,
+                            const uint32_t* __restrict__ adj, const uint32_t* __restrict__ bitmap,
+                            const ERec* __restrict__ vrec, ERec* __restrict__ erec, uint32_t rs,
+                            uint64_t* __restrict__ rev, unsigned long long* __restrict__ miss)
+{
+    for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
+        uint64_t j;
+        uint32_t c;
+        if (!run_chunk(pre, k, t, j, c)) break;
+        const uint64_t lo = (uint64_t)c * kRowChunk;
+        const uint32_t s = runs[j].src;
+        const uint64_t b = off[s], e = b + deg[s];
+        const ERec rec = vrec[s];
+        for (uint64_t q = b + lo + threadIdx.x; q < min(e, b + lo + kRowChunk); q += blockDim.x) {
+            const uint32_t y = adj[q];
+            uint64_t r = rev[q];
+            // a source target's row was rebuilt (and so was its entry for s): search it; a new edge too
+            if (r == kNoRev || ((bitmap[y >> 5] >> (y & 31)) & 1u)) {
+                const int64_t f = row_find(adj, Row{y, deg[y], 0u, off[y]}, s);
+                if (f < 0) {
+                    *miss = 1ull;
+                    continue;
+                }
+                r = (uint64_t)f;
+                rev[q] = r;
+            }
+            erec[r * rs] = rec;   // the 16-B row part (node2vec: the anchor entry behind it stays)
+            rev[r] = q;
+        }
+    }
+}
+
+void launch_rev_build(const uint64_t* off, const uint32_t* deg, const uint32_t* adj, uint64_t n, uint64_t slots,
+                      uint64_t* rev, unsigned long long* miss, hipStream_t s)
+{
+    if (n) hipLaunchKernelGGL(k_rev_owner, cu_count() * 32, 256, 0, s, off, deg, n, rev);
+    if (slots) hipLaunchKernelGGL(k_rev_build, cu_count() * 16, 256, 0, s, off, deg, adj, slots, rev, miss);
+}
+
+void launch_patch_rev(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* off, const uint32_t* deg,
+                      const uint32_t* adj, const uint32_t* bitmap, const ERec* vrec, ERec* erec, uint32_t rs,
+                      uint64_t* rev, unsigned long long* miss, hipStream_t s)
+{
+    if (k) hipLaunchKernelGGL(k_patch_rev, cu_count() * 4, 256, 0, s, runs, pre, k, off, deg, adj, bitmap, vrec, erec, rs,
+                              rev, miss);
 }
 
 // ---------------------------------------------------------------------------
@@ -3257,27 +3371,28 @@ void launch_run_chunks(const RunInfo* runs, const RowPlan* plan, uint64_t k, uin
     hipLaunchKernelGGL(k_run_chunks, grid_for(k + 1, 256), 256, 0, s, runs, plan, k, cnt);
 }
 void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint32_t* adj, const uint64_t* sofs,
-                      uint32_t* scratch, const uint64_t* anc, uint64_t* sanc, hipStream_t s)
+                      uint32_t* scratch, const uint64_t* anc, uint64_t* sanc, const uint64_t* rev, uint64_t* srev,
+                      hipStream_t s)
 {
     if (!k) return;
     if (WHARF_ROW_CHUNKED && pre)
-        hipLaunchKernelGGL(k_save_rows_c, chunk_grid(), 256, 0, s, runs, pre, k, adj, sofs, scratch, anc, sanc);
+        hipLaunchKernelGGL(k_save_rows_c, chunk_grid(), 256, 0, s, runs, pre, k, adj, sofs, scratch, anc, sanc, rev, srev);
     else
-        hipLaunchKernelGGL(k_save_rows, (unsigned)k, 256, 0, s, runs, adj, sofs, scratch, anc, sanc);
+        hipLaunchKernelGGL(k_save_rows, (unsigned)k, 256, 0, s, runs, adj, sofs, scratch, anc, sanc, rev, srev);
 }
 void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* bkeys, const uint32_t* chg,
                        const uint32_t* cf, const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs,
                        uint64_t pool_end, int insert, RowPlan* plan, uint32_t* adj, const uint64_t* sanc, uint64_t* anc,
-                       hipStream_t s)
+                       const uint64_t* srev, uint64_t* rev, hipStream_t s)
 {
     if (!k) return;
     if (WHARF_ROW_CHUNKED && pre) {
         hipLaunchKernelGGL(k_merge_rows_c, chunk_grid(), 256, 0, s, runs, pre, k, bkeys, chg, cf, scratch, sofs, relofs,
-                           pool_end, insert, plan, adj, sanc, anc);
+                           pool_end, insert, plan, adj, sanc, anc, srev, rev);
         hipLaunchKernelGGL(k_resolve_plan, grid_for(k, 256), 256, 0, s, runs, k, relofs, pool_end, plan);
     } else {
         hipLaunchKernelGGL(k_merge_rows, (unsigned)k, 256, 0, s, runs, bkeys, chg, cf, scratch, sofs, relofs,
-                           pool_end, insert, plan, adj, sanc, anc);
+                           pool_end, insert, plan, adj, sanc, anc, srev, rev);
     }
 }
 void launch_anchor_invalidate(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint64_t* off,

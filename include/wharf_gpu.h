@@ -227,7 +227,7 @@ int wharf_get_stats(const wharf_handle* h, wharf_stats* out);
  * held by the handle, by role. */
 typedef struct wharf_memory {
     uint64_t n, m;
-    uint64_t csr_bytes;             /* offsets + targets (the edge trees' content) */
+    uint64_t csr_bytes;             /* offsets + targets (the edge trees' content) + reverse-slot index */
     uint64_t records_bytes;         /* vertex + edge row records */
     uint64_t walks_bytes;           /* walk matrix + per-walk rewalk positions (the walk trees) */
     uint64_t samplers_bytes;        /* MH anchors + per-row sampler epochs (the samplers) */

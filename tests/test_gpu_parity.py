@@ -465,6 +465,9 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     monkeypatch.setenv("WHARF_N2V_LIST_ORDER", "global" if path == "sorted/global-move" else "block")
     monkeypatch.setenv("WHARF_NO_ROW_SLACK", no_slack)
     monkeypatch.setenv("WHARF_POOL_NO_HEADROOM", no_headroom)
+    # in-edge records of the sources: the reverse-slot index (default on undirected graphs; the last,
+    # directed batch drops it) or the streaming scan of the pool
+    monkeypatch.setenv("WHARF_REV", "0" if path in ("flat/move", "sorted/plain-rows", "block/slack") else "1")
     base = O.generate_batch_of_edges(50000, 1 << 13, 6, False, False)
     off, adj = O.csr_from_edges(1 << 12, base)
     batches = [(True, O.generate_batch_of_edges(800, 1 << 12, 11, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
@@ -474,6 +477,70 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     kw = dict(deterministic=True) if mode == "det" else dict(
         deterministic=False, seed=99, model=1 if mode == "node2vec" else 0, paramP=0.5, paramQ=2.0)
     _compare_stream(W, off, adj, batches, wpv=3, L=40, **kw)
+
+
+@pytest.mark.parametrize("rows", ["slack", "move", "repack", "compact"])
+@pytest.mark.parametrize("mode", ["det", "deepwalk", "node2vec"])
+def test_reverse_slot_index(W, monkeypatch, rows, mode):
+    """The in-edge records of a batch's sources patched through the reverse-slot
+    index (k_patch_rev: rev[e] = the slot of the reverse edge, carried through
+    the merge, searched for edges between sources and new edges, rebuilt after a
+    repack or compaction) instead of the streaming scan: over a stream of
+    undirected insert/delete batches (RMAT hubs: many edges between sources) the
+    corpus, counters, affected ids and CSR stay the oracle's.  The index is
+    allocated (8 B per pool slot in csr_bytes) while the graph is undirected and
+    dropped by the first directed batch, which the scan then serves."""
+    monkeypatch.setenv("WHARF_REV", "1")
+    if rows == "move":
+        monkeypatch.setenv("WHARF_NO_ROW_SLACK", "1")
+    if rows == "repack":
+        monkeypatch.setenv("WHARF_POOL_NO_HEADROOM", "1")
+    if rows == "compact":   # no room for a second pool: in-place compactions
+        monkeypatch.setenv("WHARF_REPACK_MEM_CAP", "1")
+        monkeypatch.setenv("WHARF_NO_ROW_SLACK", "1")
+        monkeypatch.setenv("WHARF_POOL_HEADROOM", "22000")
+    n = 1 << 12
+    base = O.generate_batch_of_edges(40000, 2 * n, 41, False, False)
+    off, adj = O.csr_from_edges(n, base)
+    kw = dict(deterministic=True) if mode == "det" else dict(
+        deterministic=False, seed=31, model=1 if mode == "node2vec" else 0, paramP=0.5, paramQ=2.0)
+    cfg = W.WharfConfig(walks_per_vertex=3, walk_length=30, **kw)
+    g = W.WharfMH.from_csr(off, adj, config=cfg)
+    ref = O.Engine(off, adj, wpv=3, L=30, model=cfg.model, p=cfg.paramP, q=cfg.paramQ, init=cfg.sampler_init,
+                   deterministic=cfg.deterministic, seed=cfg.seed)
+    monkeypatch.setenv("WHARF_REV", "0")
+    g0 = W.WharfMH.from_csr(off, adj, config=cfg)
+    no_rev = g0.memory_footprint(verbose=False)["csr_bytes"]
+    g0.destroy()
+    monkeypatch.setenv("WHARF_REV", "1")
+    assert g.memory_footprint(verbose=False)["csr_bytes"] >= no_rev + 8 * g.number_of_edges()
+    g.generate_initial_random_walks()
+    ref.generate()
+    assert np.array_equal(g.walks(), ref.walks())
+    stream = []
+    for b in range(4):   # throughput-latency.cpp:126,135: insert batch b, delete it again
+        e = O.generate_batch_of_edges(700, n, 60 + b, False, False)
+        stream += [(True, e), (False, e)]
+    stream.append((True, O.generate_batch_of_edges(900, n, 70, False, False)))
+    for ins, e in stream:
+        ga = (g.insert_edges_batch if ins else g.delete_edges_batch)(e, remove_dups=True)
+        ra = ref.insert_edges_batch(e) if ins else ref.delete_edges_batch(e)
+        assert np.array_equal(ga, ra)
+        assert np.array_equal(g.walks(), ref.walks())
+        assert g.stats()["steps"] == ref.steps
+    o2, a2 = g.flatten_graph()
+    o3, a3 = ref.csr()
+    assert np.array_equal(o2, o3) and np.array_equal(a2, a3)
+    # a directed batch: the graph is no longer undirected, the index is dropped and the scan takes over
+    held = g.memory_footprint(verbose=False)["csr_bytes"]
+    d = O.generate_batch_of_edges(300, n, 80, False, True)
+    assert np.array_equal(g.insert_edges_batch(d, remove_dups=True), ref.insert_edges_batch(d))
+    assert np.array_equal(g.walks(), ref.walks())
+    assert g.memory_footprint(verbose=False)["csr_bytes"] <= held - 8 * g.number_of_edges()
+    e = O.generate_batch_of_edges(500, n, 81, False, False)
+    assert np.array_equal(g.insert_edges_batch(e, remove_dups=True), ref.insert_edges_batch(e))
+    assert np.array_equal(g.walks(), ref.walks())
+    g.destroy()
 
 
 @pytest.mark.parametrize("rows", ["slack", "move", "repack"])   # rows merged in place / moved / pool repacked
