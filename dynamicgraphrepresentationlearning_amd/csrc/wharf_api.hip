@@ -106,6 +106,12 @@ struct wharf_handle {
     }
     uint32_t L = 0, wpv = 0;
     bool anchors = false, has_walks = false;
+    bool walks_poisoned = false;               // a failed re-walk left the walks half updated (until generate)
+    void check_walks() const
+    {
+        REQUIRE(!walks_poisoned, WHARF_E_STATE,
+                "the walks are incomplete after a failed update (WHARF_E_STATE); call wharf_generate");
+    }
     bool anchors_cold = true;                  // node2vec MH: no generation has filled the anchor cache yet
     uint32_t epoch = 0;
     // slack-row CSR: row v = slots [off[v], off[v] + deg[v]) of the pool (adj, erec), cap[v] reserved
@@ -163,6 +169,7 @@ struct wharf_handle {
     // and there are at most kStageMax, the first walk() of one of them stages all their rows with one
     // list gather and one copy.
     static constexpr uint64_t kStageMax = 1ull << 20;
+    static constexpr uint64_t kStagePiece = 1ull << 16;   // rows per device gather of the stage (21 MB at L = 80)
     std::vector<uint32_t> last_aff;   // ascending global ids of the last update's affected walks
     uint64_t last_aff_version = ~0ull, stage_version = ~0ull;
     std::vector<uint64_t> stage_li;   // their local indices (ascending), and their rows
@@ -251,11 +258,17 @@ struct wharf_handle {
                 if (!owned_li(last_aff[i], stage_li[i])) throw WharfError(WHARF_E_STATE, "affected walk not owned");
             count.ensure(k * 8);
             HIPCHK(hipMemcpyAsync(count.p, stage_li.data(), k * 8, hipMemcpyHostToDevice, s));
-            sel.ensure(k * L * 4);
-            launch_gather_rows(walks.as<uint32_t>(), W, L, count.as<uint64_t>(), 0, k, sel.as<uint32_t>(), s);
             stage_rows.resize(k * L);
-            HIPCHK(hipMemcpyAsync(stage_rows.data(), sel.p, k * L * 4, hipMemcpyDeviceToHost, s));
-            sync();
+            // through a bounded device buffer (k * L * 4 bytes is up to 1 GB at L = 255,
+            // kept pinned in the handle afterwards): pieces of at most kStagePiece rows
+            const uint64_t piece = std::min<uint64_t>(k, kStagePiece);
+            sel.ensure(piece * L * 4);
+            for (uint64_t f = 0; f < k; f += piece) {
+                const uint64_t c = std::min(piece, k - f);
+                launch_gather_rows(walks.as<uint32_t>(), W, L, count.as<uint64_t>() + f, 0, c, sel.as<uint32_t>(), s);
+                HIPCHK(hipMemcpyAsync(stage_rows.data() + f * L, sel.p, c * L * 4, hipMemcpyDeviceToHost, s));
+                sync();
+            }
             stage_version = walks_version;
         }
         const auto it = std::lower_bound(stage_li.begin(), stage_li.end(), li);
@@ -1058,6 +1071,9 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
         HIPCHK(hipMemcpyAsync(&naff32, boff + nb, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(&lerr, a.err, 8, hipMemcpyDeviceToHost, s));
         h->sync();
+        // a skipped entry leaves the update's walks half re-walked: the walks are marked invalid, so
+        // later reads and updates fail loudly until they are generated again
+        if (lerr) h->walks_poisoned = true;
         REQUIRE(lerr == 0, WHARF_E_STATE,
                 std::string("node2vec re-walk list: ") + ((lerr & 1) ? "an entry outside the walks" : "an entry outside its block") +
                     " was skipped; the walks of this update are incomplete");
@@ -1096,6 +1112,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         REQUIRE(h, WHARF_E_INVALID, "null handle");
         REQUIRE(m == 0 || pairs, WHARF_E_INVALID, "pairs is null");
         REQUIRE(m < (1ull << 31), WHARF_E_INVALID, "batch too large");
+        h->check_walks();
         auto t0 = std::chrono::steady_clock::now();
         h->st.affected = 0;
         h->st.batch_edges = 0;
@@ -1416,6 +1433,7 @@ int wharf_destroy_index(wharf_handle* h)
         h->walks_changed();
         h->sync();
         h->has_walks = false;
+        h->walks_poisoned = false;
     });
 }
 
@@ -1453,13 +1471,24 @@ int wharf_generate(wharf_handle* h)
                 uint32_t* ow = in_walks ? h->walks.as<uint32_t>() : owner.as<uint32_t>();
                 HIPCHK(hipMemsetAsync(ow, 0, h->pool_used * 4, h->s));
                 launch_slot_owner_fill(h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->n, ow, h->s);
-                launch_anchor_init_all(a, ow, h->pool_used, h->s);
+                // round 5: the states of hub curs with small prevs in cur order (WHARF_INIT_BY_CUR=1: on;
+                // WHARF_INIT_BY_CUR_Y / _X: the degree thresholds), on undirected graphs only
+                const char* bc = getenv("WHARF_INIT_BY_CUR");
+                const char* bcy = getenv("WHARF_INIT_BY_CUR_Y");
+                const char* bcx = getenv("WHARF_INIT_BY_CUR_X");
+                // (off by default: configs[4] first generation 1128 / 1141 ms with it, 1131 / 1107 ms without,
+                // alternated on one box, profiles/r05/init_by_cur)
+                const bool by_cur = h->symmetric && bc && *bc && atoi(bc) != 0;
+                const uint32_t ty = by_cur ? (bcy && *bcy ? (uint32_t)atoi(bcy) : 256u) : 0u;
+                const uint32_t tx = bcx && *bcx ? (uint32_t)atoi(bcx) : 256u;
+                launch_anchor_init_all(a, ow, h->pool_used, ty, tx, h->s);
                 HIPCHK(hipStreamSynchronize(h->s));   // before the owner buffer is released
                 owner.release();
             }
         }
         h->anchors_cold = false;
         h->walks_changed();
+        h->walks_poisoned = false;   // every walk is written anew
         launch_walk(a, false, h->s);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(h->ev[1], h->s));
@@ -1489,6 +1518,7 @@ int wharf_batch_walk_update(wharf_handle* h, const uint32_t* sources, uint64_t k
     return guarded(h, [&] {
         REQUIRE(h, WHARF_E_INVALID, "null handle");
         REQUIRE(k == 0 || sources, WHARF_E_INVALID, "sources is null");
+        h->check_walks();
         auto t0 = std::chrono::steady_clock::now();
         h->st.affected = 0;
         h->st.steps = h->st.accepts = h->st.last_anchor_inits = h->st.last_rewalk_passes = 0;
@@ -1565,6 +1595,7 @@ int wharf_set_shard(wharf_handle* h, uint64_t lo, uint64_t hi)
         h->cfg.shard_lo = lo;
         h->cfg.shard_hi = hi;
         h->has_walks = false;
+        h->walks_poisoned = false;   // a new walk matrix
     });
 }
 
@@ -1597,6 +1628,7 @@ int wharf_set_shard_blocks(wharf_handle* h, uint32_t part, uint32_t parts, uint3
         h->cfg.shard_lo = 0;
         h->cfg.shard_hi = 0;
         h->has_walks = false;
+        h->walks_poisoned = false;   // a new walk matrix
     });
 }
 
@@ -1638,6 +1670,7 @@ static bool no_snapshot()
 
 static uint64_t local_index(wharf_handle* h, uint64_t wid)
 {
+    h->check_walks();
     uint64_t li = 0;
     REQUIRE(h->owned_li(wid, li), WHARF_E_RANGE, "walk " + std::to_string(wid) + " is not owned by this handle");
     return li;
@@ -1709,6 +1742,7 @@ static void export_walks_impl(wharf_handle* h, uint32_t* dst, int layout, hipMem
 {
     REQUIRE(h && dst, WHARF_E_INVALID, "null argument");
     REQUIRE(layout == 0 || layout == 1, WHARF_E_INVALID, "layout must be 0 or 1");
+    h->check_walks();
     const uint64_t bytes = h->W * h->L * 4;
     if (!bytes) return;
     h->ensure_walks();
@@ -1741,6 +1775,7 @@ static void export_rows_impl(wharf_handle* h, uint64_t first, uint64_t count, ui
 {
     REQUIRE(h, WHARF_E_INVALID, "null handle");
     REQUIRE(first <= h->W && count <= h->W - first, WHARF_E_RANGE, "rows outside the handle's walks");
+    h->check_walks();
     if (!count) return;
     REQUIRE(dst, WHARF_E_INVALID, "null argument");
     h->ensure_walks();
@@ -1774,6 +1809,7 @@ int wharf_write_corpus(wharf_handle* h, const char* path, const uint32_t* wids, 
 {
     return guarded(h, [&] {
         REQUIRE(h && path, WHARF_E_INVALID, "null argument");
+        h->check_walks();
         h->ensure_walks();
         const uint64_t total = wids ? count : h->W;
         const uint64_t chunk = 1 << 20;
@@ -1823,6 +1859,7 @@ namespace {
 uint64_t build_index(wharf_handle* h, int& kb, uint64_t v0, uint64_t v1)
 {
     const uint64_t W = h->W;
+    h->check_walks();
     h->ensure_walks();
     kb = (int)std::max<uint32_t>(bits_for(h->n * h->wpv * h->L), 1);
     const int vb = (int)std::max<uint32_t>(bits_for(v1 - v0), 1);

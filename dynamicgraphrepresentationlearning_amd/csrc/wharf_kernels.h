@@ -95,7 +95,10 @@ void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStr
 void launch_source_degrees(const RunInfo* runs, uint64_t k, const ERec* vrec, uint64_t* out, hipStream_t s);
 void launch_anchor_preinit(const WalkArgs& a, const uint64_t* preoff, uint64_t k, hipStream_t s);
 void launch_slot_owner_fill(const uint64_t* off, const uint32_t* deg, uint64_t n, uint32_t* owner, hipStream_t s);
-void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t slots, hipStream_t s);
+// by_cur_y != 0 (undirected graphs): the states of hub curs (deg > by_cur_y) with small prevs
+// (deg <= by_cur_x) computed in cur order by a second kernel (k_anchor_init_by_cur)
+void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t slots, uint32_t by_cur_y,
+                            uint32_t by_cur_x, hipStream_t s);
 void launch_vrec(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* row_epoch, ERec* vrec,
                  hipStream_t s);
 void launch_erec(const uint32_t* adj, uint64_t slots, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anchors,

@@ -653,7 +653,10 @@ __global__ __launch_bounds__(256) void k_slot_owner_fill(const uint64_t* __restr
     }
 }
 
-__global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint32_t* __restrict__ owner, uint64_t slots)
+// by_cur_y / by_cur_x (round 5, undirected graphs): the states (y, x) with deg(y) > by_cur_y and
+// deg(x) <= by_cur_x are left to k_anchor_init_by_cur (0: none are)
+__global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint32_t* __restrict__ owner, uint64_t slots,
+                                                         uint32_t by_cur_y, uint32_t by_cur_x)
 {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t inits = 0;
@@ -665,10 +668,45 @@ __global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint3
             rx = load_rec(a.vrec, o - 1);
             ry = load_rec(a.vrec, y);
             need = e < rx.off + rx.deg && ry.deg != 0;   // (slots past a row's end are kGap; the test is cheap)
+            if (by_cur_y && ry.deg > by_cur_y && rx.deg <= by_cur_x) need = false;
         }
         uint32_t an = 0, cls = 0;
         anchor_compute(a, need, ry, rx, an, cls, inits);
         if (need) a.anchor[e * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+    }
+    wave_add(a.counters + 7, inits);
+}
+
+// The same anchors, for the states (y, x) whose cur y is a hub (deg > by_cur_y) and
+// whose prev x is small (deg <= by_cur_x), computed in cur order: one lane per slot
+// y -> x of y's row, so a wave's states share cur's row and the 21 proposals of each
+// land in one row the wave keeps in L2, while the small prev's filter words (one
+// line) and the search for slot x -> y in x's short row (where the entry lives) are
+// the random part.  In prev order (k_anchor_init_all, lanes of one prev's row) a
+// hub cur's proposals are ~21 random lines per state.  Line model on RMAT at
+// configs[4]'s density (scale 20): 8.46 lines per state in prev order,
+// 6.66 with the states of hub y >= 256 and x <= 256 taken here.  Undirected graphs
+// only: the state (y, x) of slot x -> y is reached through slot y -> x.
+__global__ __launch_bounds__(256) void k_anchor_init_by_cur(WalkArgs a, const uint32_t* __restrict__ owner,
+                                                            uint64_t slots, uint32_t by_cur_y, uint32_t by_cur_x)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t inits = 0;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < slots; e += stride) {
+        const uint32_t x = a.adj[e], o = owner[e];
+        bool need = x != kGap && o != 0;
+        Row rx{}, ry{};
+        if (need) {
+            ry = load_rec(a.vrec, o - 1);   // cur: the row this slot belongs to
+            rx = load_rec(a.vrec, x);
+            need = e < ry.off + ry.deg && ry.deg > by_cur_y && rx.deg <= by_cur_x && rx.deg != 0;
+        }
+        uint32_t an = 0, cls = 0;
+        anchor_compute(a, need, ry, rx, an, cls, inits);
+        if (need) {
+            const int64_t ein = row_find(a.adj, rx, ry.v);   // slot x -> y: the state's entry
+            if (ein >= 0) a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+        }
     }
     wave_add(a.counters + 7, inits);
 }
@@ -678,9 +716,13 @@ void launch_slot_owner_fill(const uint64_t* off, const uint32_t* deg, uint64_t n
     if (n) hipLaunchKernelGGL(k_slot_owner_fill, cu_count() * 32, 256, 0, s, off, deg, n, owner);
 }
 
-void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t slots, hipStream_t s)
+void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t slots, uint32_t by_cur_y,
+                            uint32_t by_cur_x, hipStream_t s)
 {
-    if (slots) hipLaunchKernelGGL(k_anchor_init_all, cu_count() * 8, 256, 0, s, a, owner, slots);
+    if (!slots) return;
+    hipLaunchKernelGGL(k_anchor_init_all, cu_count() * 8, 256, 0, s, a, owner, slots, by_cur_y, by_cur_x);
+    if (by_cur_y)
+        hipLaunchKernelGGL(k_anchor_init_by_cur, cu_count() * 8, 256, 0, s, a, owner, slots, by_cur_y, by_cur_x);
 }
 
 __global__ void k_source_degrees(const RunInfo* __restrict__ runs, uint64_t k, const ERec* __restrict__ vrec,
@@ -1634,6 +1676,9 @@ __global__ __launch_bounds__(256) void k_rewalk_sorted(WalkArgs a)
         uint32_t first = active ? p + 1 : L;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, o, 64));
+#ifdef WHARF_INIT_STATS
+        if (__lane_id() == 0 && first < L) atomicAdd(a.counters + 6, 64ull * (L - first));   // lane-slots swept
+#endif
         for (uint32_t pos = first; pos < L; pos++) {
             uint32_t val = kSent;
             if (active && pos > p && w.rc.deg) {
@@ -2727,7 +2772,10 @@ __global__ void k_filter_clear_c(const RunInfo* __restrict__ runs, const uint32_
         if (!run_chunk(pre, k, t, j, c)) break;
         const uint64_t lo = (uint64_t)c * kRowChunk;
         const uint64_t fd = fdir[runs[j].src], w0 = fd & kFiltOffMask, nw = 1ull << (fd >> kFiltOffBits);
-        for (uint64_t q = lo + threadIdx.x; q < min(nw, lo + kRowChunk); q += blockDim.x) pool[w0 + q] = 0;
+        // the run's last chunk clears every word left: a filter sized by an earlier, larger degree
+        // (deletions never shrink it) can have more words than the chunks of the rows cover
+        const uint64_t hi = c + 1 == pre[j + 1] - pre[j] ? nw : min(nw, lo + kRowChunk);
+        for (uint64_t q = lo + threadIdx.x; q < hi; q += blockDim.x) pool[w0 + q] = 0;
     }
 }
 

@@ -203,16 +203,22 @@ def _compare_stream(W, off, adj, batches, wpv=3, L=12, **kw):
     g.destroy()
 
 
-@pytest.mark.parametrize("preinit_all", ["0", "1"])
+@pytest.mark.parametrize("preinit_all", ["0", "1", "1-by-cur", "1-by-prev"])
 @pytest.mark.parametrize("init", [1, 2])   # BURNIN, WEIGHT
 def test_node2vec_anchors_up_front_or_lazily(W, monkeypatch, preinit_all, init):
     """Every anchor computed at the first generation (round 4's rule: >= 1 walk step
     per slot) or lazily by the walkers (WHARF_PREINIT_ALL=0): the same corpus,
     counters, affected ids and CSR as the oracle either way, with few walks per
     slot (wpv 1, L 20 on ~5 k slots: ~4 steps per slot) and a stream of inserts
-    and deletes, so the re-walks run into states no walker had entered."""
-    monkeypatch.setenv("WHARF_PREINIT_ALL", preinit_all)
+    and deletes, so the re-walks run into states no walker had entered.  Up
+    front, the states of hub curs with small prevs are computed in cur order
+    (k_anchor_init_by_cur; 1-by-cur: thresholds lowered so that most states go
+    that way) or all in prev order (1-by-prev: WHARF_INIT_BY_CUR=0)."""
+    monkeypatch.setenv("WHARF_PREINIT_ALL", preinit_all[0])
     monkeypatch.setenv("WHARF_NO_PREINIT", "")
+    monkeypatch.setenv("WHARF_INIT_BY_CUR", "0" if preinit_all == "1-by-prev" else "1")
+    monkeypatch.setenv("WHARF_INIT_BY_CUR_Y", "4" if preinit_all == "1-by-cur" else "")
+    monkeypatch.setenv("WHARF_INIT_BY_CUR_X", "40" if preinit_all == "1-by-cur" else "")
     base = O.generate_batch_of_edges(4000, 1 << 11, 9, False, False)
     off, adj = O.csr_from_edges(1 << 10, base)
     batches = [(True, O.generate_batch_of_edges(300, 1 << 10, 21, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES),
@@ -229,7 +235,7 @@ def test_node2vec_anchors_up_front_or_lazily(W, monkeypatch, preinit_all, init):
     g.generate_initial_random_walks()
     inits = g.stats()["last_anchor_inits"]
     g.destroy()
-    assert (inits == len(adj)) if preinit_all == "1" else (0 < inits != len(adj)), (inits, len(adj))
+    assert (inits == len(adj)) if preinit_all != "0" else (0 < inits != len(adj)), (inits, len(adj))
 
 
 def test_edge_cases_isolated_dead_ends_and_flags(W):
@@ -498,7 +504,7 @@ def test_reverse_slot_index(W, monkeypatch, rows, mode):
     if rows == "compact":   # no room for a second pool: in-place compactions
         monkeypatch.setenv("WHARF_REPACK_MEM_CAP", "1")
         monkeypatch.setenv("WHARF_NO_ROW_SLACK", "1")
-        monkeypatch.setenv("WHARF_POOL_HEADROOM", "22000")
+        monkeypatch.setenv("WHARF_POOL_HEADROOM", "45000")
     n = 1 << 12
     base = O.generate_batch_of_edges(40000, 2 * n, 41, False, False)
     off, adj = O.csr_from_edges(n, base)
@@ -707,6 +713,16 @@ def test_rewalk_list_entry_out_of_range_is_reported(W, monkeypatch):
         with pytest.raises(RuntimeError, match="outside the walks"):
             g.insert_edges_batch(b, remove_dups=True)
         monkeypatch.setenv("WHARF_TEST_CORRUPT_LIST", "0")
+        # the walks are half re-walked: reads and updates fail loudly until a new generation
+        with pytest.raises(RuntimeError, match="incomplete"):
+            g.walk(0)
+        with pytest.raises(RuntimeError, match="incomplete"):
+            g.walks()
+        with pytest.raises(RuntimeError, match="incomplete"):
+            g.delete_edges_batch(b, remove_dups=True)
+        g.generate_initial_random_walks()
+        assert g.walk(0).startswith("0 ")
+        g.delete_edges_batch(b, remove_dups=True)
         g.destroy()
 
 
