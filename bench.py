@@ -151,7 +151,7 @@ def gather_ceiling(steps_per_s: float, live):
             "source": "tools/gather_roof 3.48 coarse dep, this box, before the timed region"}
 
 
-PMC_ROUNDS = ("r04_", "r03_", "r02_", "")   # newest round's rocprofv3 summary first
+PMC_ROUNDS = ("r05_", "r04_", "r03_", "r02_", "")   # newest round's rocprofv3 summary first
 
 
 def load_traffic(tag: str):
@@ -390,7 +390,7 @@ def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrie
     # affected walk ids stay in HBM (WHARF_AFFECTED_DEVICE); the host-list
     # variant (PCIe-inclusive, the reference's return value) is timed after
     out = torch.empty(max(gs.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
-    lat, aff, gu, wu, kern, rsteps, mv, mslots = [], [], [], [], [], [], [], []
+    lat, aff, gu, wu, kern, rsteps, mv, mslots, imode = [], [], [], [], [], [], [], [], []
     for b in range(batches):
         batch = W.generate_batch_of_edges(5000, ns, b, False, False, device=dev)
         barrier()
@@ -406,6 +406,7 @@ def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrie
         rsteps.append(s2["steps"])
         mv.append(s2["last_csr_move_ms"])
         mslots.append(s2["last_moved_slots"])
+        imode.append(s2["last_in_edge_mode"])
     # rewalk points alone (apply_walk_updates = false): the scan over the whole walk matrix
     scan = []
     for b in range(scan_batches):
@@ -441,6 +442,9 @@ def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrie
            "rewalk_Gsteps_per_s": round(float(np.sum(rsteps) / np.sum(kern) / 1e6), 2),
            "generation_same_graph": gen3,
            "median_in_edge_scan_ms": round(float(np.median(mv)), 4), "pool_slots": int(np.median(mslots)),
+           # in-edge records: 0 = streaming scan of the pool (pool_slots = slots read), 1 = reverse-slot
+           # index (pool_slots = the sources' new row slots, at most)
+           "in_edge_mode": "reverse_index" if np.median(imode) >= 1 else "scan",
            "stored_positions_rank0": int(gs.number_of_walks) * args.length,
            "record_bytes": 32 if (cfg.model == W.NODE2VEC and not cfg.deterministic) else 16}
     if scan:
@@ -564,7 +568,13 @@ def streaming_rooflines(rewalk, rewalk_det, scale):
                                                4 * pos, rewalk_det["median_rewalk_kernel_ms"],
                                                "4 B per stored position")
     src = rewalk or rewalk_det
-    if src:
+    if src and src.get("in_edge_mode") == "reverse_index":
+        # k_patch_rev: per slot of the sources' new rows, its target (4 B) and reverse entry (8 B) read, the
+        # reverse slot's 16-B record and 8-B entry written
+        out["in_edge_records"] = ent("in_edge_records", "k_patch_rev (in-edge records through the reverse-slot "
+                                     "index)", 36 * src["pool_slots"], src["median_in_edge_scan_ms"],
+                                     "36 B per slot of the sources' new rows")
+    elif src:
         out["in_edge_scan"] = ent("in_edge_scan", "k_patch_in_edges (records of the batch sources' in-edges)",
                                   4 * src["pool_slots"], src["median_in_edge_scan_ms"], "4 B per pool slot")
     return out or None
@@ -574,7 +584,8 @@ def _update_stream(g, W, n, batches, mixed, out):
     """Insert batch b (and, mixed, delete it again: throughput-latency.cpp:126,135)
     for b < batches: generate_batch_of_edges(5000, n, b, false, undirected)
     (memory-throughput-latency.cpp:126-134).  Per-update device times."""
-    rec = {k: [] for k in ("ms", "graph_ms", "walk_ms", "kernel_ms", "in_edge_ms", "steps", "affected", "inits")}
+    rec = {k: [] for k in ("ms", "graph_ms", "walk_ms", "kernel_ms", "in_edge_ms", "steps", "affected", "inits",
+                           "in_edge_mode")}
     for b in range(batches):
         batch = W.generate_batch_of_edges(5000, n, b, False, False)
         for ins in ((True, False) if mixed else (True,)):
@@ -589,13 +600,15 @@ def _update_stream(g, W, n, batches, mixed, out):
             rec["steps"].append(st["steps"])
             rec["affected"].append(st["affected"])
             rec["inits"].append(st["last_anchor_inits"])
+            rec["in_edge_mode"].append(st["last_in_edge_mode"])
     med = lambda k: round(float(np.median(rec[k])), 3)
     return {"updates": len(rec["ms"]), "batch_median_ms": med("ms"), "batch_p90_ms": round(float(np.percentile(rec["ms"], 90)), 3),
             "graph_update_median_ms": med("graph_ms"), "walk_update_median_ms": med("walk_ms"),
             "rewalk_kernel_median_ms": med("kernel_ms"), "in_edge_scan_median_ms": round(float(np.median(rec["in_edge_ms"])), 4),
             "mean_affected_walks": int(np.mean(rec["affected"])), "mean_rewalk_steps": int(np.mean(rec["steps"])),
             "rewalk_Gsteps_per_s": round(float(np.sum(rec["steps"]) / np.sum(rec["walk_ms"]) / 1e6), 2),
-            "mean_anchor_inits": int(np.mean(rec["inits"]))}
+            "mean_anchor_inits": int(np.mean(rec["inits"])),
+            "in_edge_records": "reverse_index" if np.median(rec["in_edge_mode"]) >= 1 else "scan"}
 
 
 def per_gpu_of_8(args, W, torch, dev, barrier):

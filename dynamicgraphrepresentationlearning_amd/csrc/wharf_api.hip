@@ -1120,6 +1120,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->st.last_graph_update_ms = h->st.last_walk_update_ms = h->st.last_walk_kernel_ms = 0;
         h->st.last_csr_move_ms = 0;
         h->st.last_moved_slots = 0;
+        h->st.last_in_edge_mode = 0;
         if (n_affected) *n_affected = 0;
         if (m == 0) return;
         hipStream_t s = h->s;
@@ -1289,7 +1290,8 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
                                   rs, s);
         HIPCHK(hipEventRecord(h->ev[5], s));
         if (h->rev_on && !h->rev_valid) h->build_rev();   // after a repack / compaction in this batch
-        h->st.last_moved_slots = h->pool_used;
+        h->st.last_moved_slots = scan ? h->pool_used : h->start_bound;   // (insert: exact; delete: an upper bound)
+        h->st.last_in_edge_mode = scan ? 0 : 1;
         if (h->anchors) {
             // the edge set changes by the batch's changing edges only; rebuild when
             // inserts (and tombstones) push the load past 0.6

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define WHARF_ABI_VERSION 6
+#define WHARF_ABI_VERSION 7
 
 enum {
     WHARF_OK = 0,
@@ -78,9 +78,11 @@ typedef struct wharf_stats {
     double   last_total_ms;        /* host wall time of the last call */
     uint64_t hbm_bytes_walks;      /* resident bytes: walk matrix */
     uint64_t hbm_bytes_graph;      /* resident bytes: CSR + vertex records (+ anchors) */
-    double   last_csr_move_ms;     /* device time of the last update's streaming pass over the slot pool
-                                      (k_patch_in_edges: the in-edge records of the batch sources) */
-    uint64_t last_moved_slots;     /* pool slots that pass read (scanned: live, slack and dead slots alike) */
+    double   last_csr_move_ms;     /* device time of the last update's in-edge record pass (the records of the
+                                      batch sources' in-edges): k_patch_in_edges, a streaming pass over the slot
+                                      pool, or k_patch_rev through the reverse-slot index (last_in_edge_mode) */
+    uint64_t last_moved_slots;     /* slots that pass read: the whole pool (scan: live, slack and dead slots
+                                      alike), or the sources' new rows, sum of their degrees (reverse index) */
     /* slack-row CSR: row v = slots [off, off + deg) of a pool with cap >= deg reserved */
     uint64_t pool_slots;           /* slots handed out to rows (live edges + slack + rows' old places) */
     uint64_t pool_capacity;        /* slots allocated */
@@ -91,6 +93,7 @@ typedef struct wharf_stats {
     uint64_t last_anchor_inits;    /* node2vec MH: anchors (MH sampler inits) computed by the last generate/update */
     uint64_t last_rewalk_passes;   /* node2vec MH re-walk by passes (k_rewalk_park): passes of the last update,
                                       0 when the lock-step kernel ran */
+    uint64_t last_in_edge_mode;    /* 0: the last update scanned the pool for in-edges, 1: reverse-slot index */
 } wharf_stats;
 
 typedef struct wharf_handle wharf_handle;

@@ -26,13 +26,13 @@ for s in "$@"; do
             STR="python3 bench.py --steps 1 --warmup 0 --rewalk-batches 0 --det-rewalk-batches 3 --n2v-steps 0 --n2v-rewalk-batches 0 --cpu-baseline off --per-gpu-of-8 0 --gather-probes 0"
             step pmc_gen_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_walk" --output-format csv -d ${OUTDIR}/pmc_gen_fetch -o run -- $GEN
             step pmc_gen_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_walk" --output-format csv -d ${OUTDIR}/pmc_gen_write -o run -- $GEN
-            step pmc_str_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_rewalk_chunked|k_rewalk_scan|k_patch_in_edges" --output-format csv -d ${OUTDIR}/pmc_str_fetch -o run -- $STR
-            step pmc_str_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_rewalk_chunked|k_rewalk_scan|k_patch_in_edges" --output-format csv -d ${OUTDIR}/pmc_str_write -o run -- $STR
+            step pmc_str_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_rewalk_chunked|k_rewalk_scan|k_patch_in_edges|k_patch_rev" --output-format csv -d ${OUTDIR}/pmc_str_fetch -o run -- $STR
+            step pmc_str_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_rewalk_chunked|k_rewalk_scan|k_patch_in_edges|k_patch_rev" --output-format csv -d ${OUTDIR}/pmc_str_write -o run -- $STR
             # durations of exactly the launches the streaming PMC passes count
             step prof_str 600 rocprofv3 --kernel-trace --stats --output-format csv -d ${OUTDIR}/prof_str -o run -- $STR ;;
     pmcstr) STR="python3 bench.py --steps 1 --warmup 0 --rewalk-batches 0 --det-rewalk-batches 3 --n2v-steps 0 --n2v-rewalk-batches 0 --cpu-baseline off --per-gpu-of-8 0 --gather-probes 0"
-            step pmc_str_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_rewalk_chunked|k_rewalk_scan|k_patch_in_edges" --output-format csv -d ${OUTDIR}/pmc_str_fetch -o run -- $STR
-            step pmc_str_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_rewalk_chunked|k_rewalk_scan|k_patch_in_edges" --output-format csv -d ${OUTDIR}/pmc_str_write -o run -- $STR
+            step pmc_str_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_rewalk_chunked|k_rewalk_scan|k_patch_in_edges|k_patch_rev" --output-format csv -d ${OUTDIR}/pmc_str_fetch -o run -- $STR
+            step pmc_str_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_rewalk_chunked|k_rewalk_scan|k_patch_in_edges|k_patch_rev" --output-format csv -d ${OUTDIR}/pmc_str_write -o run -- $STR
             step prof_str 600 rocprofv3 --kernel-trace --stats --output-format csv -d ${OUTDIR}/prof_str -o run -- $STR ;;
     c4w10)  step c4_n2v_wpv10_shard8 600 python tools/bigscale.py --model node2vec --wpv 10 --batches 3 --mixed --no-oracle --shard 8 ;;
     c4w1)   step c4_n2v_wpv1_shard8 600 python tools/bigscale.py --model node2vec --wpv 1 --batches 3 --mixed --no-oracle --shard 8 ;;

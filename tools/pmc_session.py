@@ -20,7 +20,7 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KEEP = re.compile(r"k_walk|k_rewalk|k_patch_in_edges|k_anchor|k_det_suffix|k_park")
+KEEP = re.compile(r"k_walk|k_rewalk|k_patch_in_edges|k_patch_rev|k_anchor|k_det_suffix|k_park")
 
 
 def counter(path, kernel, name, skip=0):
@@ -104,6 +104,7 @@ def main():
             "rewalk_point_scan": summary("k_rewalk_scan_", pmc["pmc_str_fetch"], pmc["pmc_str_write"], trs),
             "deterministic_rewalk_copy": summary("k_rewalk_chunked<true", pmc["pmc_str_fetch"], pmc["pmc_str_write"], trs),
             "in_edge_scan": summary("k_patch_in_edges", pmc["pmc_str_fetch"], pmc["pmc_str_write"], trs),
+            "in_edge_records": summary("k_patch_rev", pmc["pmc_str_fetch"], pmc["pmc_str_write"], trs),
             "note": "configs[2] deterministic stream (bench.py --det-rewalk-batches 3): PMC passes and the "
                     "durations of the same launches from a --kernel-trace run of the same command"}
     for tag, v in out.items():
