@@ -25,6 +25,10 @@ using namespace wharf;
 namespace {
 
 thread_local std::string g_last_error;
+// A droppable device cache of the handle in the current call (the reverse-slot index): a failed
+// device allocation frees it and tries once more (guarded() installs the handle's reclaimer)
+thread_local bool (*g_reclaim_fn)(void*) = nullptr;
+thread_local void* g_reclaim_ctx = nullptr;
 
 struct WharfError : std::runtime_error {
     int code;
@@ -57,7 +61,12 @@ struct DevBuf {
         release();
         size_t b = std::max<size_t>(bytes, 256);
         if (slack) b += b / 16;
-        HIPCHK(hipMalloc(&p, b));
+        hipError_t e = hipMalloc(&p, b);
+        if (e == hipErrorOutOfMemory && g_reclaim_fn && g_reclaim_fn(g_reclaim_ctx)) {
+            (void)hipGetLastError();
+            e = hipMalloc(&p, b);
+        }
+        HIPCHK(e);
         cap = b;
     }
     // per-batch buffers: 1/4 headroom, so batches of varying size do not free and
@@ -131,8 +140,9 @@ struct wharf_handle {
     DevBuf sanc;                               // anchor carry: the sources' old anchor entries (k_save_rows)
     DevBuf rchunk;                             // per batch source: chunk counts, then their exclusive prefix (k_*_rows_c)
     bool symmetric = false;                    // every edge's reverse is an edge (anchor carry and rev need it)
-    DevBuf rev, srev;                          // reverse-slot index (k_patch_rev) and the sources' old entries
+    DevBuf rev, srev;                          // reverse-slot index (k_patch_rev, u32 per slot) and the sources' old entries
     bool rev_on = false, rev_valid = false;    // the index is kept / matches the pool (a repack invalidates it)
+    bool rev_tried = false;                    // the lazy build (first generation) was considered
     DevBuf park, parkc;                        // node2vec MH re-walk passes: two parked-walker lists, their counts
     DevBuf bdesc;                              // node2vec MH block re-walk: per 256-walk block, its run of the list
     uint32_t st_park_passes = 0;               // passes of the last re-walk by passes (0: lock-step kernel)
@@ -547,29 +557,38 @@ struct wharf_handle {
         if (anchors) build_filters();
         bitmap.ensure((bitmap_words() + kFilterWords) * 4);   // exact bitmap, then the Bloom filter
         sync();
-        rev_on = symmetric && rev_wanted();
+        rev_on = symmetric && rev_wanted(true);
         if (rev_on) build_rev();
     }
 
-    // The reverse-slot index (k_patch_rev) on undirected graphs, unless WHARF_REV=0; by
-    // default only when its 8 B per pool slot leave room for the walk matrix of every walk
-    // the handle may own and a margin (configs[3]: 21 GB next to a 56 GB graph and 107 GB of
-    // walks; configs[4]'s 33 GB do not fit beside its 226 GB graph: it keeps the scan)
-    bool rev_wanted() const
+    // The reverse-slot index (k_patch_rev) on undirected graphs, unless WHARF_REV=0.  By
+    // default at creation when its 4 B per pool slot leave room for the walk matrix of every
+    // walk the handle may own and a margin (configs[3]: 10 GB next to a 56-GB graph and 107 GB
+    // of walks), else at the first generation, once the walk matrix is allocated (an 8-GPU
+    // rank's shard: configs[4]'s 16 GB beside its 226-GB graph and 27-GB walk shard)
+    bool rev_wanted(bool at_creation) const
     {
-        const char* e = getenv("WHARF_REV");
-        if (e && *e) return atoi(e) != 0;
-        const uint64_t walks_all = (uint64_t)n * wpv * L * 4, margin = 16ull << 30;
-        return std::max<uint64_t>(pool_cap, 1) * 8 + walks_all + margin <= free_bytes();
+        const char* e = getenv("WHARF_REV");   // 0 off, 1 on, 2 (tests) built at the first generation
+        if (e && *e) return atoi(e) == 2 ? !at_creation : atoi(e) != 0;
+        const uint64_t walks_rest = at_creation ? (uint64_t)W * L * 4 : 0, margin = 12ull << 30;
+        return std::max<uint64_t>(pool_cap, 1) * 4 + walks_rest + margin <= free_bytes();
     }
 
+    // (a device without room for it just keeps the scan: the index is an optimisation)
     void build_rev()
     {
-        rev.ensure(std::max<uint64_t>(pool_cap, 1) * 8);
-        HIPCHK(hipMemsetAsync(rev.p, 0xFF, std::max<uint64_t>(pool_cap, 1) * 8, s));   // kNoRev
+        try {
+            rev.ensure(std::max<uint64_t>(pool_cap, 1) * 4);
+        } catch (const WharfError& e) {
+            if (e.code != WHARF_E_NOMEM) throw;
+            (void)hipGetLastError();
+            drop_rev();
+            return;
+        }
+        HIPCHK(hipMemsetAsync(rev.p, 0xFF, std::max<uint64_t>(pool_cap, 1) * 4, s));   // kNoRidx
         unsigned long long* miss = errflag.as<unsigned long long>() + 4;
         HIPCHK(hipMemsetAsync(miss, 0, 8, s));
-        launch_rev_build(off.as<uint64_t>(), deg.as<uint32_t>(), adj.as<uint32_t>(), n, pool_used, rev.as<uint64_t>(),
+        launch_rev_build(off.as<uint64_t>(), deg.as<uint32_t>(), adj.as<uint32_t>(), n, pool_used, rev.as<uint32_t>(),
                          miss, s);
         unsigned long long v = 0;
         HIPCHK(hipMemcpyAsync(&v, miss, 8, hipMemcpyDeviceToHost, s));
@@ -583,6 +602,17 @@ struct wharf_handle {
         rev_on = rev_valid = false;
         rev.release();
         srev.release();
+    }
+
+    // a device allocation failed: free the reverse-slot index (true) unless an update holds it
+    bool rev_pinned = false;
+    bool reclaim()
+    {
+        if (!rev_on || rev_pinned || !rev.p) return false;
+        (void)hipStreamSynchronize(s);
+        drop_rev();
+        rev_tried = true;   // not rebuilt lazily: the room is wanted elsewhere
+        return true;
     }
 
     // the walk matrix is allocated on first use (and re-allocated by set_shard)
@@ -753,6 +783,16 @@ void set_err(wharf_handle* h, const std::string& m)
 template <class F>
 int guarded(wharf_handle* h, F&& f)
 {
+    // the reverse-slot index is a cache: an allocation that fails for want of room drops it (the
+    // in-edge scan takes over) and is retried, unless an update is using it at that moment
+    struct Reclaim {
+        Reclaim(wharf_handle* h)
+        {
+            g_reclaim_ctx = h;
+            g_reclaim_fn = h ? +[](void* p) { return static_cast<wharf_handle*>(p)->reclaim(); } : nullptr;
+        }
+        ~Reclaim() { g_reclaim_fn = nullptr; g_reclaim_ctx = nullptr; }
+    } reclaim(h);
     try {
         if (h) HIPCHK(hipSetDevice(h->device));
         f();
@@ -841,7 +881,7 @@ void build_graph_from_keys(wharf_handle* h, uint64_t cnt, bool drop_loops, bool 
 {
     const uint64_t mm = h->unique_keys(cnt, drop_loops, 32 + std::max<uint32_t>(bits_for(h->n), 1));
     h->symmetric = symmetric_by_construction;
-    if (!symmetric_by_construction && (h->anchors || h->rev_wanted())) {   // (the anchor carry and rev ask)
+    if (!symmetric_by_construction && (h->anchors || h->rev_wanted(false))) {   // (the anchor carry and rev ask)
         unsigned long long* asym = h->errflag.as<unsigned long long>() + 3;
         HIPCHK(hipMemsetAsync(asym, 0, 8, h->s));
         launch_keys_symmetric(h->k1.as<uint64_t>(), mm, asym, h->s);
@@ -1113,6 +1153,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         REQUIRE(m == 0 || pairs, WHARF_E_INVALID, "pairs is null");
         REQUIRE(m < (1ull << 31), WHARF_E_INVALID, "batch too large");
         h->check_walks();
+        h->rev_pinned = false;
         auto t0 = std::chrono::steady_clock::now();
         h->st.affected = 0;
         h->st.batch_edges = 0;
@@ -1233,7 +1274,8 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         // reverse-slot index: carried through the merge and used for the in-edge records
         // unless a repack or compaction of this batch moved every row (then: scan, rebuild)
         const bool use_rev = h->rev_on && h->rev_valid;
-        if (use_rev) h->srev.ensure_grow(std::max<uint64_t>(saved, 1) * 8);
+        h->rev_pinned = use_rev;   // from here to the in-edge pass the index must stay (no reclaim)
+        if (use_rev) h->srev.ensure_grow(std::max<uint64_t>(saved, 1) * 4);
         // Anchor carry (node2vec MH on an undirected graph): the entries of the sources' rows travel
         // through the merge and only those whose anchor can change are reset (k_anchor_invalidate);
         // otherwise every entry of a rebuilt row starts empty.  WHARF_ANCHOR_CARRY=0 (A/B, tests).
@@ -1254,12 +1296,12 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             return rocprim::exclusive_scan(t, b, rcnt, rpre, 0u, (size_t)(k + 1), rocprim::plus<uint32_t>(), s);
         });
         launch_save_rows(h->runs.as<RunInfo>(), k, rpre, h->adj.as<uint32_t>(), sofs, h->scratch.as<uint32_t>(), anc_base,
-                         carry ? h->sanc.as<uint64_t>() : nullptr, use_rev ? h->rev.as<uint64_t>() : nullptr,
-                         use_rev ? h->srev.as<uint64_t>() : nullptr, s);
+                         carry ? h->sanc.as<uint64_t>() : nullptr, use_rev ? h->rev.as<uint32_t>() : nullptr,
+                         use_rev ? h->srev.as<uint32_t>() : nullptr, s);
         launch_merge_rows(h->runs.as<RunInfo>(), k, rpre, bkeys, h->chg.as<uint32_t>(), h->cf.as<uint32_t>(),
                           h->scratch.as<uint32_t>(), sofs, relofs, h->pool_used, insert, h->rplan.as<RowPlan>(),
                           h->adj.as<uint32_t>(), carry ? h->sanc.as<uint64_t>() : nullptr, anc_base,
-                          use_rev ? h->srev.as<uint64_t>() : nullptr, use_rev ? h->rev.as<uint64_t>() : nullptr, s);
+                          use_rev ? h->srev.as<uint32_t>() : nullptr, use_rev ? h->rev.as<uint32_t>() : nullptr, s);
         launch_commit_rows(h->runs.as<RunInfo>(), k, h->rplan.as<RowPlan>(), h->epoch, h->off.as<uint64_t>(),
                            h->deg.as<uint32_t>(), h->cap.as<uint32_t>(), h->vrec.as<ERec>(), h->row_epoch.as<uint32_t>(), s);
         h->pool_used += grow;
@@ -1275,7 +1317,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             HIPCHK(hipMemsetAsync(miss, 0, 8, s));
             launch_patch_rev(h->runs.as<RunInfo>(), k, rpre, h->off.as<uint64_t>(), h->deg.as<uint32_t>(),
                              h->adj.as<uint32_t>(), h->bitmap.as<uint32_t>(), h->vrec.as<ERec>(), h->erec.as<ERec>(), rs,
-                             h->rev.as<uint64_t>(), miss, s);
+                             h->rev.as<uint32_t>(), miss, s);
             unsigned long long v = 0;
             HIPCHK(hipMemcpyAsync(&v, miss, 8, hipMemcpyDeviceToHost, s));
             h->sync();
@@ -1289,6 +1331,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
                                   h->bitmap.as<uint32_t>() + h->bitmap_words(), h->vrec.as<ERec>(), h->erec.as<ERec>(),
                                   rs, s);
         HIPCHK(hipEventRecord(h->ev[5], s));
+        h->rev_pinned = false;
         if (h->rev_on && !h->rev_valid) h->build_rev();   // after a repack / compaction in this batch
         h->st.last_moved_slots = scan ? h->pool_used : h->start_bound;   // (insert: exact; delete: an upper bound)
         h->st.last_in_edge_mode = scan ? 0 : 1;
@@ -1448,6 +1491,13 @@ int wharf_generate(wharf_handle* h)
         HIPCHK(hipMemsetAsync(h->counters.as<unsigned long long>() + 7, 0, 8, h->s));
         h->st_park_passes = 0;
         WalkArgs a = h->walk_args();
+        // the reverse-slot index, when it did not fit at creation beside every walk: now that the
+        // walk matrix (of this handle's shard) is allocated (not timed with the generation)
+        if (!h->rev_on && !h->rev_tried && h->symmetric && h->rev_wanted(false)) {
+            h->rev_on = true;
+            h->build_rev();
+        }
+        h->rev_tried = true;
         HIPCHK(hipEventRecord(h->ev[0], h->s));
         // node2vec MH with a cold anchor cache and at least as many steps as states
         // (slots): every anchor computed up front (k_anchor_init_all), timed with the

@@ -137,12 +137,12 @@ void launch_scatter_offsets(const uint32_t* order, const uint64_t* snoff, uint64
 // source rows in chunks (`pre`: exclusive prefix of launch_run_chunks' counts; null: a workgroup per row)
 void launch_run_chunks(const RunInfo* runs, const RowPlan* plan, uint64_t k, uint32_t* cnt, hipStream_t s);
 void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint32_t* adj, const uint64_t* sofs,
-                      uint32_t* scratch, const uint64_t* anc, uint64_t* sanc, const uint64_t* rev, uint64_t* srev,
+                      uint32_t* scratch, const uint64_t* anc, uint64_t* sanc, const uint32_t* rev, uint32_t* srev,
                       hipStream_t s);
 void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* bkeys, const uint32_t* chg,
                        const uint32_t* cf, const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs,
                        uint64_t pool_end, int insert, RowPlan* plan, uint32_t* adj, const uint64_t* sanc, uint64_t* anc,
-                       const uint64_t* srev, uint64_t* rev, hipStream_t s);
+                       const uint32_t* srev, uint32_t* rev, hipStream_t s);
 void launch_anchor_invalidate(const uint64_t* bkeys, uint64_t mb, const uint32_t* chg, const uint64_t* off,
                               const uint32_t* deg, const uint32_t* adj, uint64_t* anc, const uint64_t* fdir,
                               const uint32_t* fpool, hipStream_t s);
@@ -153,13 +153,13 @@ void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, cons
                       const uint32_t* adj, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anc, hipStream_t s);
 void launch_patch_in_edges(const uint32_t* adj, uint64_t slots, const uint32_t* bitmap, const uint32_t* bloom,
                            const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s);
-// reverse-slot index (undirected graphs): rev[e] = slot of (y -> x) for slot e = (x -> y)
-constexpr uint64_t kNoRev = ~0ull;
+// reverse-slot index (undirected graphs): ridx[e] = the index of x in y's row for slot e = (x -> y)
+constexpr uint32_t kNoRidx = 0xFFFFFFFFu;
 void launch_rev_build(const uint64_t* off, const uint32_t* deg, const uint32_t* adj, uint64_t n, uint64_t slots,
-                      uint64_t* rev, unsigned long long* miss, hipStream_t s);
+                      uint32_t* ridx, unsigned long long* miss, hipStream_t s);
 void launch_patch_rev(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* off, const uint32_t* deg,
                       const uint32_t* adj, const uint32_t* bitmap, const ERec* vrec, ERec* erec, uint32_t rs,
-                      uint64_t* rev, unsigned long long* miss, hipStream_t s);
+                      uint32_t* ridx, unsigned long long* miss, hipStream_t s);
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s);
 void launch_gather_rows(const uint32_t* walks, uint64_t W, uint32_t L, const uint64_t* list, uint64_t base,
                         uint64_t count, uint32_t* out, hipStream_t s);

@@ -2520,7 +2520,7 @@ __global__ void k_plan_rows(const RunInfo* __restrict__ runs, uint64_t k, const 
 __global__ void k_save_rows(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ adj,
                             const uint64_t* __restrict__ sofs, uint32_t* __restrict__ scratch,
                             const uint64_t* __restrict__ anc, uint64_t* __restrict__ sanc,
-                            const uint64_t* __restrict__ rev, uint64_t* __restrict__ srev)
+                            const uint32_t* __restrict__ rev, uint32_t* __restrict__ srev)
 {
     const RunInfo ri = runs[blockIdx.x];
     uint32_t* __restrict__ out = scratch + sofs[blockIdx.x];
@@ -2564,7 +2564,7 @@ __global__ void k_merge_rows(const RunInfo* __restrict__ runs, const uint64_t* _
                              const uint64_t* __restrict__ relofs, uint64_t pool_end, int insert,
                              RowPlan* __restrict__ plan, uint32_t* __restrict__ adj,
                              const uint64_t* __restrict__ sanc, uint64_t* __restrict__ anc,
-                             const uint64_t* __restrict__ srev, uint64_t* __restrict__ rev)
+                             const uint32_t* __restrict__ srev, uint32_t* __restrict__ rev)
 {
     const uint64_t j = blockIdx.x;
     const RunInfo ri = runs[j];
@@ -2594,7 +2594,7 @@ __global__ void k_merge_rows(const RunInfo* __restrict__ runs, const uint64_t* _
             const uint64_t at = noff + (cf[ri.rs + t] - base) + lower_bound_u32(old, d, x);
             adj[at] = x;
             if (sanc) anc[at * kAnchorStride] = kAnchorNone64;
-            if (srev) rev[at] = kNoRev;
+            if (srev) rev[at] = kNoRidx;
         }
     }
     if (reloc) {
@@ -2655,7 +2655,7 @@ __device__ __forceinline__ bool run_chunk(const uint32_t* __restrict__ pre, uint
 __global__ void k_save_rows_c(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
                               const uint32_t* __restrict__ adj, const uint64_t* __restrict__ sofs,
                               uint32_t* __restrict__ scratch, const uint64_t* __restrict__ anc, uint64_t* __restrict__ sanc,
-                              const uint64_t* __restrict__ rev, uint64_t* __restrict__ srev)
+                              const uint32_t* __restrict__ rev, uint32_t* __restrict__ srev)
 {
     for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
         uint64_t j;
@@ -2679,7 +2679,7 @@ __global__ void k_merge_rows_c(const RunInfo* __restrict__ runs, const uint32_t*
                                const uint64_t* __restrict__ sofs, const uint64_t* __restrict__ relofs, uint64_t pool_end,
                                int insert, const RowPlan* __restrict__ plan, uint32_t* __restrict__ adj,
                                const uint64_t* __restrict__ sanc, uint64_t* __restrict__ anc,
-                               const uint64_t* __restrict__ srev, uint64_t* __restrict__ rev)
+                               const uint32_t* __restrict__ srev, uint32_t* __restrict__ rev)
 {
     for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
         uint64_t j;
@@ -2714,7 +2714,7 @@ __global__ void k_merge_rows_c(const RunInfo* __restrict__ runs, const uint32_t*
                 const uint64_t at = noff + (cf[ri.rs + e] - base) + lower_bound_u32(old, d, x);
                 adj[at] = x;
                 if (sanc) anc[at * kAnchorStride] = kAnchorNone64;
-                if (srev) rev[at] = kNoRev;
+                if (srev) rev[at] = kNoRidx;
             }
         }
         if (reloc) {
@@ -2980,101 +2980,119 @@ __global__ __launch_bounds__(1024, 8) void k_patch_in_edges(const uint32_t* __re
 // ---------------------------------------------------------------------------
 // Reverse-slot index (round 5; the survey's optional rev[e]).  On
 // an undirected graph the in-edges of a batch source s are the reverses of its
-// out-edges: the slot of (y -> s) in y's row, for y in N(s).  rev[e] (u64, one
-// per pool slot) holds, for slot e = (x -> y), the slot of (y -> x).  With it
-// the records of the sources' in-edges are patched from the sources' own rows —
-// Σ deg(s) direct record writes — instead of the streaming scan of every pool
-// slot (k_patch_in_edges, 4 B per slot: 10.9 GB per batch at configs[3]).  Kept
+// out-edges: the slot of (y -> s) in y's row, for y in N(s).  ridx[e] (u32, one
+// per pool slot) holds, for slot e = (x -> y), the index of x in y's row, so the
+// reverse slot is y.off + ridx[e], with y's row offset read from e's own edge
+// record (erec[e] caches the target's row): no random read.  With it the records
+// of the sources' in-edges are patched from the sources' own rows — Σ deg(s)
+// direct record writes — instead of the streaming scan of every pool slot
+// (k_patch_in_edges, 4 B per slot: 10.9 GB per batch at configs[3]).  An index
+// relative to the target's row survives that row moving; it changes only when
+// the row's content does, i.e. when the target is itself a batch source.  Kept
 // valid through a batch:
 //  * the entries of the sources' rows travel through k_save_rows / k_merge_rows
-//    with their edges (a new edge starts kNoRev);
+//    with their edges (a new edge starts kNoRidx);
 //  * k_patch_rev recomputes an entry whose target is itself a batch source (its
 //    row was rebuilt) or new, by a search of s in the target's new row, and
-//    writes the reverse slot's entry with its record (rev[r] = q);
-//  * a repack or compaction moves every row: the index is rebuilt from scratch
-//    (k_rev_owner + k_rev_build, one search per slot), as at creation.
+//    writes the reverse slot's entry with its record (ridx[r] = q - s.off);
+//  * a repack or compaction moves the rows but not their ridx entries: the
+//    index is rebuilt from scratch (k_rev_owner + k_rev_build, one search per
+//    slot), as at its first build.
 // Directed graphs (or batches) keep the scan.  Same records either way, so no
 // result changes (the parity suite runs both: WHARF_REV=0 / 1).
 // ---------------------------------------------------------------------------
-// pass 1 of a build: rev[e] = the owner row of slot e (one wave per row; slack slots stay kNoRev)
+// pass 1 of a build: ridx[e] = the owner row of slot e (one wave per row; slack slots stay kNoRidx)
 __global__ void k_rev_owner(const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg, uint64_t n,
-                            uint64_t* __restrict__ rev)
+                            uint32_t* __restrict__ ridx)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t v = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); v < n; v += waves) {
         const uint64_t o = off[v];
         const uint32_t d = deg[v];
-        for (uint32_t i = lane; i < d; i += 64) rev[o + i] = v;
+        for (uint32_t i = lane; i < d; i += 64) ridx[o + i] = (uint32_t)v;
     }
 }
 
-// pass 2, in place: owner x of slot e = (x -> y) -> the slot of (y -> x) (a search of x in y's row)
+// pass 2, in place: owner x of slot e = (x -> y) -> the index of x in y's row (a search)
 __global__ void k_rev_build(const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg,
-                            const uint32_t* __restrict__ adj, uint64_t slots, uint64_t* __restrict__ rev,
+                            const uint32_t* __restrict__ adj, uint64_t slots, uint32_t* __restrict__ ridx,
                             unsigned long long* __restrict__ miss)
 {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < slots; e += stride) {
-        const uint64_t x = rev[e];
-        if (x == kNoRev) continue;
+        const uint32_t x = ridx[e];
+        if (x == kNoRidx) continue;
         const uint32_t y = adj[e];
-        const int64_t r = row_find(adj, Row{y, deg[y], 0u, off[y]}, (uint32_t)x);
+        const uint64_t yo = off[y];
+        const int64_t r = row_find(adj, Row{y, deg[y], 0u, yo}, x);
         if (r < 0) *miss = 1ull;   // (a plain store: every writer writes 1) the graph is not symmetric
-        rev[e] = r < 0 ? kNoRev : (uint64_t)r;
+        ridx[e] = r < 0 ? kNoRidx : (uint32_t)((uint64_t)r - yo);
     }
 }
 
+constexpr uint32_t kPatchSub = 16;   // k_patch_rev pieces per 4096-slot chunk (256 slots: a slot per thread)
+
 // Per batch, after the sources' rows and records are committed (k_commit_rows,
 // k_erec_rows): slot q = (s -> y) of source s's new row gives its reverse r, whose
-// record becomes s's new row and whose entry points back at q.  Chunks of the
+// record becomes s's new row and whose entry points back at q.  y's row (offset,
+// degree) comes from q's own record, just rewritten by k_erec_rows.  Chunks of the
 // sources' rows dealt as in k_erec_rows_c (a hub source's row spreads over the chip).
 __global__ void k_patch_rev(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
                             const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg,
                             const uint32_t* __restrict__ adj, const uint32_t* __restrict__ bitmap,
                             const ERec* __restrict__ vrec, ERec* __restrict__ erec, uint32_t rs,
-                            uint64_t* __restrict__ rev, unsigned long long* __restrict__ miss)
+                            uint32_t* __restrict__ ridx, unsigned long long* __restrict__ miss)
 {
-    for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
+    // piece t: 1/kPatchSub of run j's chunk c — one slot per thread, so the dependent loads of
+    // a batch's few chunks (configs[2]: ~500) are spread over kPatchSub times as many workgroups
+    for (uint64_t t = blockIdx.x;; t += gridDim.x) {
         uint64_t j;
         uint32_t c;
-        if (!run_chunk(pre, k, t, j, c)) break;
-        const uint64_t lo = (uint64_t)c * kRowChunk;
+        if (!run_chunk(pre, k, t / kPatchSub, j, c)) break;
+        const uint64_t lo = (uint64_t)c * kRowChunk + (t % kPatchSub) * (kRowChunk / kPatchSub);
         const uint32_t s = runs[j].src;
         const uint64_t b = off[s], e = b + deg[s];
+        if (b + lo >= e) continue;
         const ERec rec = vrec[s];
-        for (uint64_t q = b + lo + threadIdx.x; q < min(e, b + lo + kRowChunk); q += blockDim.x) {
-            const uint32_t y = adj[q];
-            uint64_t r = rev[q];
+        for (uint64_t q = b + lo + threadIdx.x; q < min(e, b + lo + kRowChunk / kPatchSub); q += blockDim.x) {
+            const Row ry = load_rec(erec, q * rs);   // the target y and its (new) row
+            uint32_t x = ridx[q];
             // a source target's row was rebuilt (and so was its entry for s): search it; a new edge too
-            if (r == kNoRev || ((bitmap[y >> 5] >> (y & 31)) & 1u)) {
-                const int64_t f = row_find(adj, Row{y, deg[y], 0u, off[y]}, s);
+            if (x == kNoRidx || ((bitmap[ry.v >> 5] >> (ry.v & 31)) & 1u)) {
+                const int64_t f = row_find(adj, ry, s);
                 if (f < 0) {
                     *miss = 1ull;
                     continue;
                 }
-                r = (uint64_t)f;
-                rev[q] = r;
+                x = (uint32_t)((uint64_t)f - ry.off);
+                ridx[q] = x;
             }
+            const uint64_t r = ry.off + x;
             erec[r * rs] = rec;   // the 16-B row part (node2vec: the anchor entry behind it stays)
-            rev[r] = q;
+            ridx[r] = (uint32_t)(q - b);
         }
     }
 }
 
 void launch_rev_build(const uint64_t* off, const uint32_t* deg, const uint32_t* adj, uint64_t n, uint64_t slots,
-                      uint64_t* rev, unsigned long long* miss, hipStream_t s)
+                      uint32_t* ridx, unsigned long long* miss, hipStream_t s)
 {
-    if (n) hipLaunchKernelGGL(k_rev_owner, cu_count() * 32, 256, 0, s, off, deg, n, rev);
-    if (slots) hipLaunchKernelGGL(k_rev_build, cu_count() * 16, 256, 0, s, off, deg, adj, slots, rev, miss);
+    if (n) hipLaunchKernelGGL(k_rev_owner, cu_count() * 32, 256, 0, s, off, deg, n, ridx);
+    if (slots) hipLaunchKernelGGL(k_rev_build, cu_count() * 16, 256, 0, s, off, deg, adj, slots, ridx, miss);
 }
 
 void launch_patch_rev(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* off, const uint32_t* deg,
                       const uint32_t* adj, const uint32_t* bitmap, const ERec* vrec, ERec* erec, uint32_t rs,
-                      uint64_t* rev, unsigned long long* miss, hipStream_t s)
+                      uint32_t* ridx, unsigned long long* miss, hipStream_t s)
 {
-    if (k) hipLaunchKernelGGL(k_patch_rev, cu_count() * 4, 256, 0, s, runs, pre, k, off, deg, adj, bitmap, vrec, erec, rs,
-                              rev, miss);
+    // workgroups per CU (each deals 4096-slot chunks of the sources' rows; A/B: WHARF_PATCH_REV_WG)
+    static const int per_cu = [] {
+        const char* e = getenv("WHARF_PATCH_REV_WG");
+        return e && *e ? std::max(1, atoi(e)) : 16;
+    }();
+    if (k) hipLaunchKernelGGL(k_patch_rev, cu_count() * per_cu, 256, 0, s, runs, pre, k, off, deg, adj, bitmap, vrec,
+                              erec, rs, ridx, miss);
 }
 
 // ---------------------------------------------------------------------------
@@ -3419,7 +3437,7 @@ void launch_run_chunks(const RunInfo* runs, const RowPlan* plan, uint64_t k, uin
     hipLaunchKernelGGL(k_run_chunks, grid_for(k + 1, 256), 256, 0, s, runs, plan, k, cnt);
 }
 void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint32_t* adj, const uint64_t* sofs,
-                      uint32_t* scratch, const uint64_t* anc, uint64_t* sanc, const uint64_t* rev, uint64_t* srev,
+                      uint32_t* scratch, const uint64_t* anc, uint64_t* sanc, const uint32_t* rev, uint32_t* srev,
                       hipStream_t s)
 {
     if (!k) return;
@@ -3431,7 +3449,7 @@ void launch_save_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, cons
 void launch_merge_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* bkeys, const uint32_t* chg,
                        const uint32_t* cf, const uint32_t* scratch, const uint64_t* sofs, const uint64_t* relofs,
                        uint64_t pool_end, int insert, RowPlan* plan, uint32_t* adj, const uint64_t* sanc, uint64_t* anc,
-                       const uint64_t* srev, uint64_t* rev, hipStream_t s)
+                       const uint32_t* srev, uint32_t* rev, hipStream_t s)
 {
     if (!k) return;
     if (WHARF_ROW_CHUNKED && pre) {

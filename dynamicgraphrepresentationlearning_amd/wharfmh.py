@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes as C
 import dataclasses
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -72,8 +73,22 @@ class WharfConfig:
 class WharfMH:
     """Streaming random-walk engine: CSR snapshot + position-major walk matrix in HBM."""
 
+    # every live handle (weakly): destroy_all() frees the device memory of handles a caller lost
+    # track of, e.g. a test that failed with its handle still referenced by the traceback
+    _live: "weakref.WeakSet[WharfMH]" = weakref.WeakSet()
+
+    @classmethod
+    def destroy_all(cls) -> int:
+        n = 0
+        for g in list(cls._live):
+            if getattr(g, "_h", None):
+                g.destroy()
+                n += 1
+        return n
+
     def __init__(self, n: int, m: int = 0, offsets=None, edges=None, config: WharfConfig | None = None,
                  device: int = 0, _handle=None):
+        WharfMH._live.add(self)
         # a copy: set_shard records the shard here, not in the caller's object
         self.config = dataclasses.replace(config) if config is not None else WharfConfig()
         self._cfg = self.config.to_c()

@@ -16,3 +16,15 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(REPO, "tests", "golden")
+
+
+@pytest.fixture(autouse=True)
+def _free_gpu_handles(request):
+    """After every GPU test, free the device memory of any handle still alive (a failed
+    test's handle stays referenced by its traceback and would starve the next tests)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    mod = sys.modules.get("dynamicgraphrepresentationlearning_amd.wharfmh")
+    if mod is not None:
+        mod.WharfMH.destroy_all()

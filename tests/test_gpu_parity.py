@@ -485,7 +485,7 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     _compare_stream(W, off, adj, batches, wpv=3, L=40, **kw)
 
 
-@pytest.mark.parametrize("rows", ["slack", "move", "repack", "compact"])
+@pytest.mark.parametrize("rows", ["slack", "slack-lazy", "move", "repack", "compact"])
 @pytest.mark.parametrize("mode", ["det", "deepwalk", "node2vec"])
 def test_reverse_slot_index(W, monkeypatch, rows, mode):
     """The in-edge records of a batch's sources patched through the reverse-slot
@@ -494,9 +494,10 @@ def test_reverse_slot_index(W, monkeypatch, rows, mode):
     repack or compaction) instead of the streaming scan: over a stream of
     undirected insert/delete batches (RMAT hubs: many edges between sources) the
     corpus, counters, affected ids and CSR stay the oracle's.  The index is
-    allocated (8 B per pool slot in csr_bytes) while the graph is undirected and
+    allocated (4 B per pool slot in csr_bytes) while the graph is undirected and
     dropped by the first directed batch, which the scan then serves."""
-    monkeypatch.setenv("WHARF_REV", "1")
+    rev_on = "2" if rows == "slack-lazy" else "1"   # 2: built at the first generation, not at creation
+    monkeypatch.setenv("WHARF_REV", rev_on)
     if rows == "move":
         monkeypatch.setenv("WHARF_NO_ROW_SLACK", "1")
     if rows == "repack":
@@ -518,9 +519,9 @@ def test_reverse_slot_index(W, monkeypatch, rows, mode):
     g0 = W.WharfMH.from_csr(off, adj, config=cfg)
     no_rev = g0.memory_footprint(verbose=False)["csr_bytes"]
     g0.destroy()
-    monkeypatch.setenv("WHARF_REV", "1")
-    assert g.memory_footprint(verbose=False)["csr_bytes"] >= no_rev + 8 * g.number_of_edges()
+    monkeypatch.setenv("WHARF_REV", rev_on)
     g.generate_initial_random_walks()
+    assert g.memory_footprint(verbose=False)["csr_bytes"] >= no_rev + 4 * g.number_of_edges()
     ref.generate()
     assert np.array_equal(g.walks(), ref.walks())
     stream = []
@@ -542,7 +543,7 @@ def test_reverse_slot_index(W, monkeypatch, rows, mode):
     d = O.generate_batch_of_edges(300, n, 80, False, True)
     assert np.array_equal(g.insert_edges_batch(d, remove_dups=True), ref.insert_edges_batch(d))
     assert np.array_equal(g.walks(), ref.walks())
-    assert g.memory_footprint(verbose=False)["csr_bytes"] <= held - 8 * g.number_of_edges()
+    assert g.memory_footprint(verbose=False)["csr_bytes"] <= held - 4 * g.number_of_edges()
     e = O.generate_batch_of_edges(500, n, 81, False, False)
     assert np.array_equal(g.insert_edges_batch(e, remove_dups=True), ref.insert_edges_batch(e))
     assert np.array_equal(g.walks(), ref.walks())
