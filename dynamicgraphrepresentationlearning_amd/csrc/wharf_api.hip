@@ -143,6 +143,7 @@ struct wharf_handle {
     DevBuf rev, srev;                          // reverse-slot index (k_patch_rev, u32 per slot) and the sources' old entries
     bool rev_on = false, rev_valid = false;    // the index is kept / matches the pool (a repack invalidates it)
     bool rev_tried = false;                    // the lazy build (first generation) was considered
+    static constexpr uint64_t kRevMinPool = 1ull << 28;   // slots: below, the in-edge scan is as fast
     DevBuf park, parkc;                        // node2vec MH re-walk passes: two parked-walker lists, their counts
     DevBuf bdesc;                              // node2vec MH block re-walk: per 256-walk block, its run of the list
     uint32_t st_park_passes = 0;               // passes of the last re-walk by passes (0: lock-step kernel)
@@ -570,6 +571,9 @@ struct wharf_handle {
     {
         const char* e = getenv("WHARF_REV");   // 0 off, 1 on, 2 (tests) built at the first generation
         if (e && *e) return atoi(e) == 2 ? !at_creation : atoi(e) != 0;
+        // a small pool is scanned faster than its sources' in-edges are patched one by one
+        // (configs[2], 96 M slots: scan 0.155 ms, index 0.23 ms; configs[3], 2.6 G: 2.35 vs 0.9 ms)
+        if (pool_cap < kRevMinPool) return false;
         const uint64_t walks_rest = at_creation ? (uint64_t)W * L * 4 : 0, margin = 12ull << 30;
         return std::max<uint64_t>(pool_cap, 1) * 4 + walks_rest + margin <= free_bytes();
     }
@@ -881,7 +885,9 @@ void build_graph_from_keys(wharf_handle* h, uint64_t cnt, bool drop_loops, bool 
 {
     const uint64_t mm = h->unique_keys(cnt, drop_loops, 32 + std::max<uint32_t>(bits_for(h->n), 1));
     h->symmetric = symmetric_by_construction;
-    if (!symmetric_by_construction && (h->anchors || h->rev_wanted(false))) {   // (the anchor carry and rev ask)
+    const char* rv = getenv("WHARF_REV");
+    const bool rev_may = rv && *rv ? atoi(rv) != 0 : mm >= wharf_handle::kRevMinPool;
+    if (!symmetric_by_construction && (h->anchors || rev_may)) {   // (the anchor carry and the reverse index ask)
         unsigned long long* asym = h->errflag.as<unsigned long long>() + 3;
         HIPCHK(hipMemsetAsync(asym, 0, 8, h->s));
         launch_keys_symmetric(h->k1.as<uint64_t>(), mm, asym, h->s);

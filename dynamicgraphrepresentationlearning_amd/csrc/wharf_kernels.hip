@@ -3031,8 +3031,6 @@ __global__ void k_rev_build(const uint64_t* __restrict__ off, const uint32_t* __
     }
 }
 
-constexpr uint32_t kPatchSub = 16;   // k_patch_rev pieces per 4096-slot chunk (256 slots: a slot per thread)
-
 // Per batch, after the sources' rows and records are committed (k_commit_rows,
 // k_erec_rows): slot q = (s -> y) of source s's new row gives its reverse r, whose
 // record becomes s's new row and whose entry points back at q.  y's row (offset,
@@ -3044,18 +3042,17 @@ __global__ void k_patch_rev(const RunInfo* __restrict__ runs, const uint32_t* __
                             const ERec* __restrict__ vrec, ERec* __restrict__ erec, uint32_t rs,
                             uint32_t* __restrict__ ridx, unsigned long long* __restrict__ miss)
 {
-    // piece t: 1/kPatchSub of run j's chunk c — one slot per thread, so the dependent loads of
-    // a batch's few chunks (configs[2]: ~500) are spread over kPatchSub times as many workgroups
-    for (uint64_t t = blockIdx.x;; t += gridDim.x) {
+    // (pieces of 256 slots — one per thread — instead of the 4096-slot chunks were slower: the
+    // chunk lookup's dependent loads then run once per 256 slots; configs[3] 0.9 -> 1.55 ms)
+    for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
         uint64_t j;
         uint32_t c;
-        if (!run_chunk(pre, k, t / kPatchSub, j, c)) break;
-        const uint64_t lo = (uint64_t)c * kRowChunk + (t % kPatchSub) * (kRowChunk / kPatchSub);
+        if (!run_chunk(pre, k, t, j, c)) break;
+        const uint64_t lo = (uint64_t)c * kRowChunk;
         const uint32_t s = runs[j].src;
         const uint64_t b = off[s], e = b + deg[s];
-        if (b + lo >= e) continue;
         const ERec rec = vrec[s];
-        for (uint64_t q = b + lo + threadIdx.x; q < min(e, b + lo + kRowChunk / kPatchSub); q += blockDim.x) {
+        for (uint64_t q = b + lo + threadIdx.x; q < min(e, b + lo + kRowChunk); q += blockDim.x) {
             const Row ry = load_rec(erec, q * rs);   // the target y and its (new) row
             uint32_t x = ridx[q];
             // a source target's row was rebuilt (and so was its entry for s): search it; a new edge too
