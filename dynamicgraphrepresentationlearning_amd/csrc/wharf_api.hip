@@ -1013,6 +1013,8 @@ void walk_update(wharf_handle* h, uint64_t k, uint32_t flags, uint32_t* affected
                 h->bdesc.ensure(((h->W + 255) / 256) * 8);
                 a.bdesc = h->bdesc.as<uint64_t>();
             }
+            const char* pg = getenv("WHARF_N2V_PLAN_GROUP");   // A/B: 1024-walk groups in the plan's list
+            a.plan_group = !a.bdesc && pg && *pg && atoi(pg) != 0;
             const char* no_stab = getenv("WHARF_NO_START_TABLE");   // A/B and tests: binary search at every start
             if (!a.scan_only && k && !(no_stab && atoi(no_stab))) {
                 // start states (x, prev): x a batch source, prev an in-neighbour of it, so at most

@@ -63,6 +63,7 @@ struct WalkArgs {
     int ret_first;               // node2vec MH, WEIGHT, 1/p the unique heaviest weight: return-first inits (walk_step)
     unsigned long long* err;     // re-walk list consumers: bit 0 an entry out of range, bit 1 an entry outside its block
     int stage;                   // node2vec re-walk launch: 0 plan + consumer, 1 plan only, 2 consumer only
+    int plan_group;              // k_rewalk_plan_lean: bin the 4 blocks of a workgroup together (A/B, no bdesc)
 };
 
 __host__ __device__ __forceinline__ ShardMap shard_map(const WalkArgs& a)

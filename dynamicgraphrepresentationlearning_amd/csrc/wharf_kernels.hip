@@ -1444,9 +1444,13 @@ __global__ __launch_bounds__(1024, 8) void k_rewalk_plan_lean(WalkArgs a)
         if (li < W) a.aff[li] = (uint8_t)p;
         if (a.scan_only) continue;
         const uint32_t key = (li < W && p + 1 < L) ? p : 255u;   // re-walking: something after the point
+        // plan_group (A/B): the workgroup's 1024 walks binned as one group (bins of block 0; the
+        // others stay empty and scan to zeros), so a wave's 64 entries span a narrower range of
+        // rewalk points over 4 KB of row instead of 1 KB
+        const uint32_t gb = a.plan_group ? 0u : sb;
         s_bin[sb][tl] = 0;
         __syncthreads();
-        atomicAdd(&s_bin[sb][key], 1u);
+        atomicAdd(&s_bin[gb][key], 1u);
         __syncthreads();
         const uint32_t c = s_bin[sb][tl];
         uint32_t incl = c;                                 // exclusive scan of the block's 256 bins
@@ -1461,14 +1465,14 @@ __global__ __launch_bounds__(1024, 8) void k_rewalk_plan_lean(WalkArgs a)
         for (uint32_t w = 0; w < wv; w++) before += s_wsum[sb][w];
         s_bin[sb][tl] = before + incl - c;
         __syncthreads();
-        const uint32_t nact = s_bin[sb][255];              // entries ranked before the "none" bin
-        if (tl == 0) s_ticket[sb] = nact ? atomicAdd(a.counters + 2, (1ull << 40) | nact) : 0ull;
+        const uint32_t nact = s_bin[gb][255];              // entries ranked before the "none" bin
+        if (tl == 0 && gb == sb) s_ticket[sb] = nact ? atomicAdd(a.counters + 2, (1ull << 40) | nact) : 0ull;
         __syncthreads();
         const uint64_t blk = (base >> 8) + sb;
         if (tl == 0 && a.bdesc && (blk << 8) < W) a.bdesc[blk] = (s_ticket[sb] & kListMask) | ((uint64_t)nact << 40);
         if (key != 255u) {
-            const uint32_t rank = atomicAdd(&s_bin[sb][key], 1u);
-            const uint64_t tk = s_ticket[sb];
+            const uint32_t rank = atomicAdd(&s_bin[gb][key], 1u);
+            const uint64_t tk = s_ticket[gb];
             const uint32_t at = ((tk >> 40) & 1u) ? nact - 1 - rank : rank;
             a.defer[(tk & kListMask) + at] = li | ((uint64_t)p << 56);
         }

@@ -471,6 +471,9 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     monkeypatch.setenv("WHARF_N2V_LIST_ORDER", "global" if path == "sorted/global-move" else "block")
     monkeypatch.setenv("WHARF_NO_ROW_SLACK", no_slack)
     monkeypatch.setenv("WHARF_POOL_NO_HEADROOM", no_headroom)
+    # node2vec plan: the re-walk list binned per 256-walk block (default) or per 1024-walk workgroup
+    monkeypatch.setenv("WHARF_N2V_PLAN_GROUP", "1" if path in ("sorted/lazy-inits", "park/slack", "sorted/move-lazy")
+                       else "0")
     # in-edge records of the sources: the reverse-slot index (default on undirected graphs; the last,
     # directed batch drops it) or the streaming scan of the pool
     monkeypatch.setenv("WHARF_REV", "0" if path in ("flat/move", "sorted/plain-rows", "block/slack") else "1")
