@@ -576,6 +576,37 @@ def test_node2vec_anchor_reset_with_prev_row(W, monkeypatch, rows, init):
                     deterministic=False, seed=4321)
 
 
+@pytest.mark.parametrize("rows", ["slack", "repack"])
+def test_hub_row_cut_down_then_regrown(W, monkeypatch, rows):
+    """a hub row cut down by deletions keeps the neighbour filter its
+    old degree sized (deletions never shrink it), so after a repack recaps the row
+    the filter can hold more words than the row's chunks cover; the refill clears
+    every word of it.  A hub loses most of its edges, the pool is repacked
+    (WHARF_POOL_NO_HEADROOM=1) or the row merged in its slack, then the hub gains
+    edges again: node2vec MH corpus, counters, affected ids and CSR stay the
+    oracle's (the filter is exact for negatives either way; stale bits would only
+    cost extra edge-hash probes, which the counts below do not see)."""
+    monkeypatch.setenv("WHARF_POOL_NO_HEADROOM", "1" if rows == "repack" else "0")
+    n = 1 << 11
+    base = O.generate_batch_of_edges(30000, 2 * n, 23, False, False)
+    off, adj = O.csr_from_edges(n, base)
+    deg = np.diff(off.astype(np.int64))
+    hub = int(np.argmax(deg))
+    nbrs = adj[off[hub]:off[hub + 1]].astype(np.uint32)
+    cut = nbrs[: (len(nbrs) * 7) // 8]                        # most of the hub's row, both directions
+    cut_pairs = np.concatenate([np.stack([np.full_like(cut, hub), cut], 1), np.stack([cut, np.full_like(cut, hub)], 1)])
+    back = cut[: len(cut) // 3]
+    back_pairs = np.concatenate([np.stack([np.full_like(back, hub), back], 1), np.stack([back, np.full_like(back, hub)], 1)])
+    R, A = O.REMOVE_DUPS, O.APPLY_WALK_UPDATES
+    batches = [(False, cut_pairs.astype(np.uint32), R | A),
+               (True, O.generate_batch_of_edges(300, n, 41, False, False), R | A),   # rows move, the pool repacks
+               (True, back_pairs.astype(np.uint32), R | A),
+               (True, O.generate_batch_of_edges(300, n, 42, False, False), R | A)]
+    assert len(nbrs) > 100, len(nbrs)
+    _compare_stream(W, off, adj, batches, wpv=3, L=30, model=1, paramP=0.5, paramQ=2.0, sampler_init=2,
+                    deterministic=False, seed=99)
+
+
 @pytest.mark.parametrize("mode", ["det", "node2vec"])
 def test_pool_compaction_without_room_for_a_second_pool(W, monkeypatch, mode):
     """When the pool runs out of headroom and the device cannot hold a second
