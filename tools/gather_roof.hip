@@ -10,6 +10,8 @@
 //   stream the same bytes read sequentially (HBM streaming ceiling)
 //   dep_64B_block / dep_128B_block: each gather reads the whole aligned 64-B /
 //   128-B block around its slot (calibrates what one 16-B gather fetches)
+//   dep_store2B / dep_store1B: a 2-B / 1-B store per step (does the store cost scale with bytes?)
+//   dep_store_at_end: the lane's 79 steps held in VGPRs, written after its last gather
 //
 // Second argument: table memory kind — "coarse" (hipMalloc, default),
 // "uncached" (hipDeviceMallocUncached: requests bypass L2 line fills) or
@@ -51,7 +53,9 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ t, uin
     uint32_t x = mix((uint32_t)li);
     uint32_t b0 = 0, b1 = 0, b2 = 0;   // mode 8: 4-step store buffer
     __shared__ uint32_t tile[16 * 256];   // modes 11/12: 16 steps x 256 lanes staged in LDS
-    for (int p = 0; p < L; p++) {
+    uint32_t hold[MODE == 16 ? 79 : 1];   // mode 16: the walk in registers (L = 79, fully unrolled)
+#pragma unroll
+    for (int p = 0; p < (MODE == 16 ? 79 : L); p++) {
         uint64_t slot;
         if (MODE == 4) {                                                          // dep + Philox4x32-10 per step
             uint32_t c0 = (uint32_t)li, c1 = x, c2 = (uint32_t)p, c3 = 0, k0 = 0x5EED, k1 = 0;
@@ -90,7 +94,13 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ t, uin
         } else {
             r = t[slot];
         }
-        if (MODE == 8) {          // dep, one 16-B store per 4 steps ([p/4][W] x uint4 layout)
+        if (MODE == 16) {         // dep, the lane's whole walk kept in VGPRs, written after its last gather
+            hold[p] = r.x;   // written after the loop
+        } else if (MODE == 15) {  // dep, a 2-B store per step (half the write bytes)
+            reinterpret_cast<uint16_t*>(out)[(uint64_t)p * W + li] = (uint16_t)r.x;
+        } else if (MODE == 17) {  // dep, a 1-B store per step
+            reinterpret_cast<uint8_t*>(out)[(uint64_t)p * W + li] = (uint8_t)r.x;
+        } else if (MODE == 8) {          // dep, one 16-B store per 4 steps ([p/4][W] x uint4 layout)
             if ((p & 3) == 0) b0 = r.x;
             else if ((p & 3) == 1) b1 = r.x;
             else if ((p & 3) == 2) b2 = r.x;
@@ -122,6 +132,11 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ t, uin
         }
         x = (MODE == 0 || MODE >= 3) ? mix(r.y ^ x) : x + r.y;
     }
+    if (MODE == 16) {
+        __asm__ volatile("" ::: "memory");   // keep the compiler from moving the stores back between the gathers
+#pragma unroll
+        for (int k = 0; k < 79; k++) out[(uint64_t)k * W + li] = hold[k];
+    }
 }
 
 int main(int argc, char** argv)
@@ -143,11 +158,12 @@ int main(int argc, char** argv)
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
-    const char* names[15] = {"dep", "indep", "stream", "dep_nt", "dep_philox", "dep_4B", "dep_8B", "dep_nostore",
+    const char* names[18] = {"dep", "indep", "stream", "dep_nt", "dep_philox", "dep_4B", "dep_8B", "dep_nostore",
                              "dep_store16B_per_4", "dep_store_same_row", "dep_store_nt",
-                             "dep_store_lds16_tiled", "dep_store_lds16_rows", "dep_64B_block", "dep_128B_block"};
+                             "dep_store_lds16_tiled", "dep_store_lds16_rows", "dep_64B_block", "dep_128B_block",
+                             "dep_store2B", "dep_store_at_end", "dep_store1B"};
     for (int rep = 0; rep < 2; rep++)
-        for (int mode = 0; mode < 15; mode++) {
+        for (int mode = 0; mode < 18; mode++) {
             if (only && std::strcmp(only, names[mode]) != 0) continue;
             CHK(hipEventRecord(a));
             if (mode == 0) hipLaunchKernelGGL(k_gather<0>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
@@ -165,6 +181,9 @@ int main(int argc, char** argv)
             if (mode == 12) hipLaunchKernelGGL(k_gather<12>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 13) hipLaunchKernelGGL(k_gather<13>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             if (mode == 14) hipLaunchKernelGGL(k_gather<14>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 15) hipLaunchKernelGGL(k_gather<15>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 16) hipLaunchKernelGGL(k_gather<16>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
+            if (mode == 17) hipLaunchKernelGGL(k_gather<17>, (unsigned)((W + 255) / 256), 256, 0, 0, t, n, out, W, L);
             CHK(hipEventRecord(b));
             CHK(hipEventSynchronize(b));
             float ms;
