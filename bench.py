@@ -704,14 +704,28 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
     (distributed.gather_corpus_chunked): chunks of at most `budget_bytes` land
     in one reused buffer, local rows are read from the handle per chunk.  Timed
     pass (the chunk is dropped), then a checked pass: the checksum of everything
-    every rank received equals the sum of the ranks' local checksums."""
-    from dynamicgraphrepresentationlearning_amd.distributed import corpus_checksum, gather_corpus_chunked, \
-        local_corpus_checksum, shard_size
+    every rank received equals the sum of the ranks' local checksums.
+
+    `budget_bytes` is this rank's own (from its free memory); the rows per chunk
+    are agreed (minimum over the ranks) before anything is allocated, and every
+    fallible local step is agreed before the next collective (distributed.agree),
+    so a rank that fails makes every rank raise RankFailure instead of hanging."""
+    from dynamicgraphrepresentationlearning_amd.distributed import agree, agree_min, corpus_checksum, \
+        gather_corpus_chunked, injected_fault, local_corpus_checksum, shard_size
     on_dev = comm_dev != "cpu"
-    K = max(1, int(budget_bytes // (world * L * 4)))
-    stage = None if on_dev else torch.empty((K, L), dtype=torch.int32, device=f"cuda:{dev}")
+    K_local = max(1, int(budget_bytes // (world * L * 4)))
+    K = max(1, agree_min(K_local, device=comm_dev) if dist else K_local)
+    stage, err = None, None
+    try:
+        injected_fault("gather", rank)
+        if not on_dev:
+            stage = torch.empty((K, L), dtype=torch.int32, device=f"cuda:{dev}")
+    except Exception as ex:   # noqa: BLE001 (agreed: every rank abandons the gather)
+        err = ex
+    agree(err, "corpus gather setup", device=comm_dev)
 
     def read_local(first, count, out):
+        injected_fault("gather_read", rank)
         if on_dev:
             g.export_walk_rows(first, count, out)
         else:   # gloo rehearsal: rows staged through the device buffer to host memory
@@ -728,7 +742,7 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
            "backend": "nccl (RCCL over xGMI)" if on_dev else "gloo (host staging)",
            "walks": sum(shard_size(sh) for sh in shards) * wpv,
            "corpus_bytes": sum(shard_size(sh) for sh in shards) * wpv * L * 4,
-           "rows_per_rank_per_chunk": K,
+           "rows_per_rank_per_chunk": K, "rows_per_rank_this_rank_budget": K_local,
            "buffer_bytes": K * world * L * 4, "chunks": st["chunks"], "ms": round(ms_all, 2),
            "bytes_received_rank0": int(st["bytes_received"]),
            "GBps_received_per_rank": round(st["bytes_received"] / (ms_all * 1e-3) / 1e9, 1) if ms_all else None}
@@ -740,7 +754,12 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
                 acc.add_(corpus_checksum(chunk[r0:r0 + c], g0, L))
 
         gather_corpus_chunked(read_local, shards, n, wpv, L, K, sink, device=comm_dev)
-        mine = local_corpus_checksum(read_local, shards[rank], n, wpv, L, K, device=comm_dev)
+        mine, err = None, None
+        try:
+            mine = local_corpus_checksum(read_local, shards[rank], n, wpv, L, K, device=comm_dev)
+        except Exception as ex:   # noqa: BLE001
+            err = ex
+        agree(err, "local corpus checksum", device=comm_dev)
         tot = mine.clone()
         if dist:
             dist.all_reduce(tot)
@@ -767,6 +786,41 @@ JOBS = {
 }
 
 
+class _Phase:
+    """`with phase("name"):` runs one rank's local, fallible part of a job phase
+    (no collective inside) and then agrees the outcome with every rank
+    (distributed.agree): if any rank failed, every rank raises RankFailure at
+    the end of the same phase, so no rank is left waiting in a later collective.
+    WHARF_TEST_FAIL="<rank>:<phase>" (phase = the name's first word) makes that
+    rank's phase fail at its end, as if its body had raised."""
+
+    def __init__(self, dist, comm_dev, rank):
+        self.dist, self.comm_dev, self.rank = dist, comm_dev, rank
+
+    def __call__(self, name):
+        self.name = name
+        return self
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, ev, tb):
+        from dynamicgraphrepresentationlearning_amd.distributed import agree, injected_fault
+        if et is not None and not issubclass(et, Exception):
+            return False   # KeyboardInterrupt / SystemExit: not a job failure
+        if ev is None:
+            try:
+                injected_fault(self.name.split()[0], self.rank)
+            except RuntimeError as ex:
+                ev = ex
+                if not self.dist:
+                    raise
+        if self.dist:
+            agree(ev, self.name, device=self.comm_dev)   # raises RankFailure on every rank if any failed
+            return False
+        return False       # one process, no peers: the exception propagates as it is
+
+
 def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrier):
     """One of BASELINE's 8-GPU jobs on the ranks of this run: the graph built on
     every rank (replicated, wharfmh.h:275,761 shard by walk), the rank's walk
@@ -775,8 +829,15 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
     undirected) (configs[4]: each inserted, then deleted,
     throughput-latency.cpp:126,135).  Per update: barrier, the rank's wall time,
     max over ranks.  configs[3] also runs, on rank 0 alone, every walk on one
-    GPU over the same graph: the 1-GPU time the job divides."""
-    from dynamicgraphrepresentationlearning_amd.distributed import balanced_shards, block_shards, shard_size
+    GPU over the same graph: the 1-GPU time the job divides.
+
+    Every fallible step (build, each generation, the gather, each update, the
+    one-GPU leg) is a phase whose outcome all ranks agree on before the next
+    collective: a rank that fails (e.g. out of device memory) makes every rank
+    return {"error", "failed_rank", "phase"} together instead of leaving its
+    peers inside a barrier."""
+    from dynamicgraphrepresentationlearning_amd.distributed import RankFailure, balanced_shards, block_shards, \
+        injected_fault, shard_size
     spec = JOBS[name]
     scale = spec["scale"] + args.job_scale_delta
     samples = spec["samples"] >> (-args.job_scale_delta) if args.job_scale_delta < 0 else spec["samples"]
@@ -785,25 +846,28 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
     node2vec = spec["model"] == "node2vec"
     cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, model=W.NODE2VEC if node2vec else W.DEEPWALK,
                         paramP=0.5, paramQ=2.0, deterministic=False, seed=0x5EED)
+    phase = _Phase(dist, comm_dev, rank)
     g = None
     try:
         t0 = time.time()
-        g = W.WharfMH.from_rmat(n, samples, 2 * n, seed=4, config=cfg, device=dev)
-        if args.job_shards == "blocks":   # 64 Ki-vertex blocks round-robin: every rank the same mix
-            shards = block_shards(n, parts, args.job_block_bits)
-        else:                               # contiguous ranges with equal non-isolated vertex counts
-            shards = balanced_shards(np.diff(g.offsets().astype(np.int64)), parts)
-        g.apply_shard(shards[rank])
+        with phase("build"):
+            g = W.WharfMH.from_rmat(n, samples, 2 * n, seed=4, config=cfg, device=dev)
+            if args.job_shards == "blocks":   # 64 Ki-vertex blocks round-robin: every rank the same mix
+                shards = block_shards(n, parts, args.job_block_bits)
+            else:                               # contiguous ranges with equal non-isolated vertex counts
+                shards = balanced_shards(np.diff(g.offsets().astype(np.int64)), parts)
+            g.apply_shard(shards[rank])
         build_s = time.time() - t0
         gen = []
-        for _ in range(2):   # first (node2vec: every anchor initialised) and warm generation
+        for i in range(2):   # first (node2vec: every anchor initialised) and warm generation
             barrier()
-            t1 = time.perf_counter()
-            g.generate_initial_random_walks()
-            torch.cuda.synchronize(dev)
-            wall = (time.perf_counter() - t1) * 1e3
-            st = g.stats()
-            gen.append((wall, st["last_walk_kernel_ms"], st["steps"], st["last_anchor_inits"]))
+            with phase(f"generation {i}"):
+                t1 = time.perf_counter()
+                g.generate_initial_random_walks()
+                torch.cuda.synchronize(dev)
+                wall = (time.perf_counter() - t1) * 1e3
+                st = g.stats()
+                gen.append((wall, st["last_walk_kernel_ms"], st["steps"], st["last_anchor_inits"]))
         gmax = _max_over_ranks(torch, dist, comm_dev, [gen[0][0], gen[1][0], gen[0][1], gen[1][1]])
         gsum = _sum_over_ranks(torch, dist, comm_dev, [gen[1][2], gen[0][3]])
         rec = {"workload": f"BASELINE {name}: {spec['desc']}; RMAT scale {scale}, {samples} undirected samples "
@@ -823,26 +887,29 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
                "device_bytes_rank0": g.memory_footprint(verbose=False)["total_bytes"]}
         if args.job_gather and dist:
             free = torch.cuda.mem_get_info(dev)[0] if comm_dev != "cpu" else (8 << 30)
+            # this rank's budget; corpus_gather_record agrees the chunk (minimum over the ranks)
             budget = max(64 << 20, min(args.gather_chunk_bytes, free // 4))
             rec["corpus_allgatherv"] = corpus_gather_record(args, torch, dist, g, shards[:world], n, 10, 80, dev,
                                                             comm_dev, world, rank, barrier, budget)
-        ids = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
+        with phase("ids"):
+            ids = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
         per = {k: [] for k in ("wall", "graph", "walk", "in_edge", "steps", "affected", "inits")}
         for b in range(args.job_batches):
-            batch = W.generate_batch_of_edges(5000, n, b, False, False, device=dev)
             for ins in ((True, False) if spec["mixed"] else (True,)):
                 barrier()
-                t1 = time.perf_counter()
-                (g.insert_edges_batch if ins else g.delete_edges_batch)(batch, remove_dups=True, out=ids)
-                torch.cuda.synchronize(dev)
-                per["wall"].append((time.perf_counter() - t1) * 1e3)
-                st = g.stats()
-                per["graph"].append(st["last_graph_update_ms"])
-                per["walk"].append(st["last_walk_update_ms"])
-                per["in_edge"].append(st["last_csr_move_ms"])
-                per["steps"].append(st["steps"])
-                per["affected"].append(st["affected"])
-                per["inits"].append(st["last_anchor_inits"])
+                with phase(f"batch {b} {'insert' if ins else 'delete'}"):
+                    batch = W.generate_batch_of_edges(5000, n, b, False, False, device=dev)
+                    t1 = time.perf_counter()
+                    (g.insert_edges_batch if ins else g.delete_edges_batch)(batch, remove_dups=True, out=ids)
+                    torch.cuda.synchronize(dev)
+                    per["wall"].append((time.perf_counter() - t1) * 1e3)
+                    st = g.stats()
+                    per["graph"].append(st["last_graph_update_ms"])
+                    per["walk"].append(st["last_walk_update_ms"])
+                    per["in_edge"].append(st["last_csr_move_ms"])
+                    per["steps"].append(st["steps"])
+                    per["affected"].append(st["affected"])
+                    per["inits"].append(st["last_anchor_inits"])
         if per["wall"]:
             job_ms = _max_over_ranks(torch, dist, comm_dev, per["wall"])
             steps = _sum_over_ranks(torch, dist, comm_dev, per["steps"])
@@ -865,26 +932,30 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
         if spec["split"] == "ranks" and world > 1 and args.job_one_gpu:
             # the same graph (after this job's batches) with every walk on rank 0's GPU
             one = None
-            if rank == 0:
-                g.set_shard(0, n)
-                g.generate_initial_random_walks()
-                g.generate_initial_random_walks()
-                st = g.stats()
-                ids = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
-                o = _update_stream_from(g, W, n, args.job_batches, args.job_batches, spec["mixed"], ids, dev)
-                one = {"walks": g.number_of_walks, "generation_ms": round(st["last_walk_kernel_ms"], 2),
-                       "batch_median_ms": o["batch_median_ms"], "graph_update_median_ms": o["graph_update_median_ms"],
-                       "walk_update_median_ms": o["walk_update_median_ms"],
-                       "batches": f"generate_batch_of_edges(5000, n, b, false, undirected), "
-                                  f"b = {args.job_batches}..{2 * args.job_batches - 1}"}
             barrier()
+            with phase("one_gpu"):
+                if rank == 0:
+                    g.set_shard(0, n)
+                    g.generate_initial_random_walks()
+                    g.generate_initial_random_walks()
+                    st = g.stats()
+                    ids = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
+                    o = _update_stream_from(g, W, n, args.job_batches, args.job_batches, spec["mixed"], ids, dev)
+                    one = {"walks": g.number_of_walks, "generation_ms": round(st["last_walk_kernel_ms"], 2),
+                           "batch_median_ms": o["batch_median_ms"], "graph_update_median_ms": o["graph_update_median_ms"],
+                           "walk_update_median_ms": o["walk_update_median_ms"],
+                           "batches": f"generate_batch_of_edges(5000, n, b, false, undirected), "
+                                      f"b = {args.job_batches}..{2 * args.job_batches - 1}"}
             if one is not None:
                 rec["one_gpu_same_graph"] = one
                 if "batch_median_ms" in rec:
                     rec["batch_ratio_one_gpu_to_job"] = round(one["batch_median_ms"] / rec["batch_median_ms"], 2)
                 rec["generation_ratio_one_gpu_to_job"] = round(one["generation_ms"] / rec["generation_kernel_ms_max"], 2)
         return rec
-    except Exception as ex:   # noqa: BLE001 (a job that does not fit is reported, the headline still prints)
+    except RankFailure as ex:   # every rank is here together: the job is abandoned, the headline still prints
+        log(f"[rank {rank}] job {name} abandoned: {ex}")
+        return {"error": str(ex)[:500], "failed_rank": ex.rank, "phase": ex.phase}
+    except Exception as ex:   # noqa: BLE001 (one process: a job that does not fit is reported)
         log(f"[rank {rank}] job {name} failed: {ex}")
         return {"error": str(ex)[:500]}
     finally:
@@ -973,9 +1044,13 @@ def main():
     # corpus reassembly for the downstream consumer: bounded full-mesh all-gatherv over RCCL (not timed in `value`)
     corpus = None
     if dist:
+        from dynamicgraphrepresentationlearning_amd.distributed import RankFailure
         free = torch.cuda.mem_get_info(dev)[0] if comm_dev != "cpu" else (8 << 30)
-        corpus = corpus_gather_record(args, torch, dist, g, shards, n, wpv, args.length, dev, comm_dev, world, rank,
-                                      barrier, max(64 << 20, min(args.gather_chunk_bytes, free // 4)))
+        try:   # the budget is this rank's; the chunk is agreed over the ranks inside
+            corpus = corpus_gather_record(args, torch, dist, g, shards, n, wpv, args.length, dev, comm_dev, world,
+                                          rank, barrier, max(64 << 20, min(args.gather_chunk_bytes, free // 4)))
+        except RankFailure as ex:   # every rank abandons the gather together; the headline still prints
+            corpus = {"error": str(ex)[:500], "failed_rank": ex.rank, "phase": ex.phase}
     g.destroy()
 
     # strong scaling beside the weak line: configs[1] exactly (10 walks per vertex) split N ways

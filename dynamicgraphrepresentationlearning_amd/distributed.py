@@ -26,12 +26,83 @@ Two forms:
     its row runs, and the buffer is reused.  Local rows come from a callback
     (WharfMH.export_walk_rows: one device gather per chunk), so neither the
     corpus nor the rank's own walk-major copy is ever whole in memory.
+
+Collective safety: a rank that fails between collectives must not leave its
+peers waiting inside one.  `agree` is the one rule every multi-rank phase
+follows (bench.py's jobs, the chunked gather): each rank runs its local,
+fallible work, then all ranks meet in ONE small all-reduce that says whether
+any rank failed; if one did, every rank raises RankFailure (carrying the
+failing rank's error) at the same point, so the job is abandoned together.
+Sizes that shape a collective (the gather's rows per chunk) are agreed the
+same way (all-reduce MIN) instead of trusted to be equal.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
+
+
+class RankFailure(RuntimeError):
+    """Raised on EVERY rank when any rank failed a phase (see `agree`)."""
+
+    def __init__(self, rank: int, phase: str, message: str):
+        super().__init__(f"rank {rank} failed in {phase}: {message}")
+        self.rank = rank
+        self.phase = phase
+        self.message = message
+
+
+def _dist_active(group=None) -> bool:
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
+def agree(err, phase: str, group=None, device="cpu"):
+    """Collective: every rank reports whether its part of `phase` failed (err =
+    the exception or None).  Returns only if no rank failed; otherwise raises
+    RankFailure(first failing rank, phase, its error text) on every rank.
+    Without an initialised process group it re-raises err."""
+    if not _dist_active(group):
+        if err is not None:
+            raise err
+        return
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    t = torch.tensor([rank if err is not None else world], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    src = int(t.item())
+    if src == world:
+        return
+    msg = [f"{type(err).__name__}: {str(err)[:400]}" if err is not None else None]
+    dist.broadcast_object_list(msg, src=src if group is None else dist.get_global_rank(group, src), group=group,
+                               device=torch.device(device) if device != "cpu" else None)
+    raise RankFailure(src, phase, msg[0]) from err
+
+
+def agree_min(value: int, group=None, device="cpu") -> int:
+    """Collective: the minimum of `value` over the ranks (a size every rank must share)."""
+    if not _dist_active(group):
+        return int(value)
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return int(t.item())
+
+
+def injected_fault(phase: str, rank: int):
+    """Test hook: WHARF_TEST_FAIL="<rank>:<phase>[,...]" makes that rank raise at
+    the start of that phase (tests/test_distributed_cpu.py drives a one-rank
+    failure through bench.py's jobs and the chunked gather)."""
+    spec = os.environ.get("WHARF_TEST_FAIL")
+    if spec and f"{rank}:{phase}" in spec.split(","):
+        raise RuntimeError(f"injected fault (WHARF_TEST_FAIL) at {phase} on rank {rank}")
 
 
 def balanced_shards(deg: np.ndarray, parts: int):
@@ -181,7 +252,13 @@ def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per
         chunk = [R, L] tensor (valid until sink returns) and segments =
         [(chunk_row, count, global_walk_id_first)] covering its R rows.
     At most rows_per_rank * world rows (rows_per_rank on a sending-only rank)
-    are resident.  Returns {"chunks", "bytes_received", "bytes_sent"} of this rank.
+    are resident.  rows_per_rank may differ between ranks (each derives it from
+    its own free memory): the chunk size used is the minimum over the ranks,
+    agreed before the first exchange, because chunk boundaries and receive
+    sizes must be the same on every rank.  A failure on one rank (buffer,
+    read_local, sink) is agreed before the next exchange and raises
+    RankFailure on every rank.  Returns {"chunks", "rows_per_rank",
+    "bytes_received", "bytes_sent"} of this rank.
     """
     import torch
     import torch.distributed as dist
@@ -192,12 +269,17 @@ def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per
     owns = [shard_size(sh) * wpv for sh in shards]
     if len(owns) != world:
         raise ValueError(f"{len(owns)} shards for a world of {world}")
-    K = max(1, int(rows_per_rank))
+    K = max(1, agree_min(max(1, int(rows_per_rank)), group, device))
     nchunks = -(-max(owns) // K) if max(owns) else 0
     receives = root is None or rank == root
-    buf = torch.empty((K * (world if receives else 1), L), dtype=dtype, device=device)
+    buf, err = None, None
+    try:
+        buf = torch.empty((K * (world if receives else 1), L), dtype=dtype, device=device)
+    except Exception as ex:   # noqa: BLE001 (agreed below: every rank abandons the gather together)
+        err = ex
+    agree(err, "corpus gather buffer", group, device)
     cuda = buf.is_cuda
-    stats = {"chunks": nchunks, "bytes_received": 0, "bytes_sent": 0}
+    stats = {"chunks": nchunks, "rows_per_rank": K, "bytes_received": 0, "bytes_sent": 0}
     for c in range(nchunks):
         parts = [(min(c * K, own), min((c + 1) * K, own)) for own in owns]
         cnt = [b - a for a, b in parts]
@@ -208,8 +290,12 @@ def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per
                 acc += cnt[g]
         my0 = base[rank] if receives else 0
         mine = buf[my0:my0 + cnt[rank]]
-        if cnt[rank]:
-            read_local(parts[rank][0], cnt[rank], mine)
+        if cnt[rank] and err is None:
+            try:
+                read_local(parts[rank][0], cnt[rank], mine)
+            except Exception as ex:   # noqa: BLE001
+                err = ex
+        agree(err, f"corpus gather chunk {c}", group, device)
         ops = []
         for peer in range(world):
             if peer == rank:
@@ -233,9 +319,13 @@ def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per
                 if cnt[g]:
                     for lf, k, gf in shard_rows_to_global(sh, n, parts[g][0], cnt[g]):
                         segs.append((base[g] + lf - parts[g][0], k, gf))
-            sink(buf[:sum(cnt)], segs)
-            if cuda:
-                torch.cuda.current_stream(buf.device).synchronize()
+            try:
+                sink(buf[:sum(cnt)], segs)
+                if cuda:
+                    torch.cuda.current_stream(buf.device).synchronize()
+            except Exception as ex:   # noqa: BLE001 (agreed before the next exchange or at the end)
+                err = ex
+    agree(err, "corpus gather sink", group, device)
     return stats
 
 

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Same-box A/B of bench.py's per_gpu_of_8 cases (configs[3] shard 0 of 8, configs[3] all walks on one GPU,
+# configs[4] node2vec shard 0 of 8), alternated REPS times over the variants named on the command line:
+#   head         this tree, defaults
+#   head@VAR=v   this tree with one environment setting (e.g. head@WHARF_REV=0)
+#   tree:<dir>   another tree's bench.py + package (e.g. tools/ab/r04, built from an older commit)
+# Logs: gpurun_out/${TAG:-per8}_<variant>_<rep>.log; a failing run ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-per8}
+REPS=${REPS:-2}
+ARGS="--steps 1 --warmup 0 --rewalk-batches 0 --det-rewalk-batches 0 --n2v-steps 0 --cpu-baseline off --gather-probes 0 ${EXTRA:-}"
+for rep in $(seq 1 $REPS); do
+    for v in "$@"; do
+        name=${v%%@*}; envset=""; [ "$name" != "$v" ] && envset=${v#*@}
+        dir=.; case $name in tree:*) dir=${name#tree:};; esac
+        tag=$(echo "$v" | tr '@=:/' '____')
+        log=gpurun_out/${TAG}_${tag}_${rep}.log
+        ( [ -n "$envset" ] && export "$envset"; cd "$dir" && timeout -k 10 420 python -u bench.py $ARGS ) > "$log" 2>&1
+        rc=$?
+        echo "== $v rep $rep rc=$rc"
+        grep '^per_gpu_of_8 ' "$log" | \
+            python -c "
+import json,sys
+for l in sys.stdin:
+    if not l.startswith('per_gpu_of_8'): continue
+    k, j = l.split(': ', 1); d = json.loads(j)
+    print(k[13:], {x: d.get(x) for x in ('first_generation_ms', 'generation_ms', 'batch_median_ms', 'graph_update_median_ms', 'walk_update_median_ms', 'rewalk_kernel_median_ms', 'in_edge_records', 'device_bytes')})"
+        [ $rc -eq 0 ] || exit $rc
+    done
+done
