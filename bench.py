@@ -335,6 +335,79 @@ def cpu_baseline_same_shape(args, W, torch, dev, extrapolated):
     return rec
 
 
+def cpu_baseline_deterministic_same_shape(args, W, torch, dev, extrapolated=None):
+    """The reference's default mode (config::deterministic_mode = true,
+    globals.h:29) MEASURED at the workload's walk shape:
+    walks_per_vertex and L of the GPU line (10 x 80), DeepWalk, on the same
+    scale --cpu-scale RMAT graph as cpu_baseline_same_shape (configs[1]'s
+    per-vertex density); generation, then one 10k-edge insert batch
+    generate_batch_of_edges(5000, n, 0, false, undirected) with the walk update
+    applied (memory-throughput-latency.cpp:126-148).  The GPU runs the same
+    graph and batch in the same mode beside it (bit-exact with the reference
+    in this mode, tests/test_gpu_parity.py).  `extrapolated` (the configs[2]
+    sample at 1 x 24, scaled linearly) is kept as a secondary field."""
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness) or args.cpu_scale <= 0:
+        return extrapolated
+    cores = cpu_cores(args.cpu_threads)
+    S = args.cpu_scale
+    ns = 1 << S
+    samples = args.samples >> max(0, args.scale - S)
+    cfg = W.WharfConfig(walks_per_vertex=args.wpv, walk_length=args.length, model=W.DEEPWALK, deterministic=True)
+    g = W.WharfMH.from_rmat(ns, samples, 2 * ns, seed=args.seed, config=cfg, device=dev)
+    m = g.number_of_edges()
+    g.generate_initial_random_walks()
+    g.generate_initial_random_walks()
+    st = g.stats()
+    batch = W.generate_batch_of_edges(5000, ns, 0, False, False, device=dev)
+    out = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    aff = g.insert_edges_batch(batch, remove_dups=True, out=out)
+    torch.cuda.synchronize(dev)
+    gpu_ms = (time.perf_counter() - t1) * 1e3
+    st2 = g.stats()
+    gpu = {"generation_kernel_ms": round(st["last_walk_kernel_ms"], 3), "walk_steps": st["steps"],
+           "insert_batch_ms": round(gpu_ms, 3), "insert_batch_affected_walks": int(len(aff)),
+           "insert_batch_graph_update_ms": round(st2["last_graph_update_ms"], 3),
+           "insert_batch_walk_update_ms": round(st2["last_walk_update_ms"], 3),
+           "insert_batch_rewalk_steps": st2["steps"]}
+    g.destroy()
+    cmd = [harness, "cfg", str(args.wpv), str(args.length), "deepwalk", str(args.paramP), str(args.paramQ), "weight",
+           "1", "42", "graph-rmat", str(samples), str(2 * ns), str(args.seed), str(ns), "time-gen", "1",
+           "time-upd", "5000", "0", "0", "1"]
+    log(f"cpu_baseline_deterministic (same shape): reference harness, {cores} threads: {' '.join(cmd[1:])}")
+    try:
+        r = subprocess.run(cmd, env=dict(os.environ, NUM_THREADS=str(cores)), capture_output=True, text=True,
+                           timeout=args.cpu_timeout)
+    except subprocess.TimeoutExpired:
+        log("cpu_baseline_deterministic (same shape): harness timed out")
+        return extrapolated
+    gen = re.search(r"time-gen seconds=([0-9.]+)", r.stdout)
+    upd = re.search(r"time-upd seconds=([0-9.]+) edges=(\d+) affected=(\d+)", r.stdout)
+    if r.returncode != 0 or not gen or not upd:
+        log("cpu_baseline_deterministic (same shape): harness failed", r.returncode, r.stderr[-500:])
+        return extrapolated
+    cpu_batch_ms = float(upd.group(1)) * 1e3
+    rec = {"kind": "reference", "cores": cores, "host": host_cpus(),
+           "sample": f"reference WharfMH, deterministic mode, MEASURED at the workload's walk shape "
+                     f"(walks_per_vertex={args.wpv}, L={args.length}, DeepWalk) on RMAT scale {S} (n={ns}, "
+                     f"{samples} undirected samples = configs[1]'s per-vertex density, m={m}): generation, then "
+                     f"one insert batch generate_batch_of_edges(5000, n, 0, false, undirected) with the walk "
+                     f"update applied",
+           "graph": {"scale": S, "n": ns, "m": m, "samples": samples, "seed": args.seed},
+           "generation_seconds": float(gen.group(1)),
+           "generation_walk_steps_per_s": round(gpu["walk_steps"] / float(gen.group(1)), 1),
+           "insert_batch_ms": round(cpu_batch_ms, 1), "insert_batch_edges": int(upd.group(2)),
+           "insert_batch_affected_walks": int(upd.group(3)),
+           "gpu_same_graph": gpu,
+           "gpu_over_cpu_insert_batch": round(cpu_batch_ms / gpu_ms, 1),
+           "affected_walks_equal": int(upd.group(3)) == int(len(aff))}
+    if extrapolated:
+        rec["configs2_extrapolation"] = extrapolated
+    return rec
+
+
 def cpu_baseline_deterministic(args, batches=3):
     """The reference's default mode (config::deterministic_mode = true,
     globals.h:29) on the reference CPU path: configs[2]'s graph, generation and
@@ -698,7 +771,8 @@ def _per_rank(torch, dist, comm_dev, vals, world):
     return [o.tolist() for o in out]
 
 
-def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev, world, rank, barrier, budget_bytes):
+def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev, world, rank, barrier, budget_bytes,
+                         mem=None):
     """The corpus reassembled for the downstream consumer (yskip,
     vertex-classification.cpp:142-158) by the bounded full-mesh all-gatherv
     (distributed.gather_corpus_chunked): chunks of at most `budget_bytes` land
@@ -726,6 +800,8 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
 
     def read_local(first, count, out):
         injected_fault("gather_read", rank)
+        if mem is not None:   # the chunk buffer (and, after the first chunk, RCCL's buffers) are live here
+            mem.probe("corpus gather")
         if on_dev:
             g.export_walk_rows(first, count, out)
         else:   # gloo rehearsal: rows staged through the device buffer to host memory
@@ -784,6 +860,31 @@ JOBS = {
                      desc="friendster-sized RMAT, node2vec p=0.5 q=2 MH WEIGHT, walks_per_vertex=10, L=80, "
                           "insert/delete pairs; rank g runs start-vertex shard g of 8"),
 }
+
+
+class _MemLow:
+    """Lowest free device memory (hipMemGetInfo) seen at the probes of a job:
+    after the build, each generation, each gather chunk (buffer and RCCL
+    buffers live) and each update -- the job's peak footprint on this rank."""
+
+    def __init__(self, torch, dev, on):
+        self.torch, self.dev, self.on = torch, dev, on
+        self.low, self.total, self.where = None, None, None
+
+    def probe(self, where):
+        if not self.on:
+            return
+        free, total = self.torch.cuda.mem_get_info(self.dev)
+        if self.low is None or free < self.low:
+            self.low, self.where = free, where
+        self.total = total
+
+    def record(self):
+        if self.low is None:
+            return None
+        return {"min_free_bytes": int(self.low), "total_bytes": int(self.total),
+                "peak_used_bytes": int(self.total - self.low), "at": self.where,
+                "source": "hipMemGetInfo (torch.cuda.mem_get_info) at the job's phase boundaries and gather chunks"}
 
 
 class _Phase:
@@ -847,6 +948,7 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
     cfg = W.WharfConfig(walks_per_vertex=10, walk_length=80, model=W.NODE2VEC if node2vec else W.DEEPWALK,
                         paramP=0.5, paramQ=2.0, deterministic=False, seed=0x5EED)
     phase = _Phase(dist, comm_dev, rank)
+    mem = _MemLow(torch, dev, comm_dev != "cpu" or dist is None)
     g = None
     try:
         t0 = time.time()
@@ -857,6 +959,7 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
             else:                               # contiguous ranges with equal non-isolated vertex counts
                 shards = balanced_shards(np.diff(g.offsets().astype(np.int64)), parts)
             g.apply_shard(shards[rank])
+            mem.probe("build")
         build_s = time.time() - t0
         gen = []
         for i in range(2):   # first (node2vec: every anchor initialised) and warm generation
@@ -868,6 +971,7 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
                 wall = (time.perf_counter() - t1) * 1e3
                 st = g.stats()
                 gen.append((wall, st["last_walk_kernel_ms"], st["steps"], st["last_anchor_inits"]))
+                mem.probe(f"generation {i}")
         gmax = _max_over_ranks(torch, dist, comm_dev, [gen[0][0], gen[1][0], gen[0][1], gen[1][1]])
         gsum = _sum_over_ranks(torch, dist, comm_dev, [gen[1][2], gen[0][3]])
         rec = {"workload": f"BASELINE {name}: {spec['desc']}; RMAT scale {scale}, {samples} undirected samples "
@@ -890,7 +994,7 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
             # this rank's budget; corpus_gather_record agrees the chunk (minimum over the ranks)
             budget = max(64 << 20, min(args.gather_chunk_bytes, free // 4))
             rec["corpus_allgatherv"] = corpus_gather_record(args, torch, dist, g, shards[:world], n, 10, 80, dev,
-                                                            comm_dev, world, rank, barrier, budget)
+                                                            comm_dev, world, rank, barrier, budget, mem)
         with phase("ids"):
             ids = torch.empty(max(g.number_of_walks, 1), dtype=torch.int32, device=f"cuda:{dev}")
         per = {k: [] for k in ("wall", "graph", "walk", "in_edge", "steps", "affected", "inits")}
@@ -910,6 +1014,7 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
                     per["steps"].append(st["steps"])
                     per["affected"].append(st["affected"])
                     per["inits"].append(st["last_anchor_inits"])
+                    mem.probe(f"batch {b} {'insert' if ins else 'delete'}")
         if per["wall"]:
             job_ms = _max_over_ranks(torch, dist, comm_dev, per["wall"])
             steps = _sum_over_ranks(torch, dist, comm_dev, per["steps"])
@@ -951,6 +1056,13 @@ def multi_gpu_job(args, name, W, torch, dev, world, rank, dist, comm_dev, barrie
                 if "batch_median_ms" in rec:
                     rec["batch_ratio_one_gpu_to_job"] = round(one["batch_median_ms"] / rec["batch_median_ms"], 2)
                 rec["generation_ratio_one_gpu_to_job"] = round(one["generation_ms"] / rec["generation_kernel_ms_max"], 2)
+        low = mem.record()
+        if low:   # every rank's peak: the job fits where the largest does
+            peaks = _per_rank(torch, dist, comm_dev, [float(low["peak_used_bytes"]), float(low["min_free_bytes"])],
+                              world)
+            low["peak_used_bytes_per_rank"] = [int(p[0]) for p in peaks]
+            low["min_free_bytes_per_rank"] = [int(p[1]) for p in peaks]
+            rec["device_memory"] = low
         return rec
     except RankFailure as ex:   # every rank is here together: the job is abandoned, the headline still prints
         log(f"[rank {rank}] job {name} abandoned: {ex}")
@@ -1162,7 +1274,13 @@ def main():
                     log(f"cpu_baseline (same shape) failed: {ex}")
             line["cpu_baseline"] = same or ext
             if args.cpu_baseline in ("auto", "reference") and args.det_rewalk_batches > 0:
-                line["cpu_baseline_deterministic"] = cpu_baseline_deterministic(args)
+                ext_det = cpu_baseline_deterministic(args, batches=1)
+                try:
+                    line["cpu_baseline_deterministic"] = cpu_baseline_deterministic_same_shape(args, W, torch, dev,
+                                                                                               ext_det)
+                except Exception as ex:   # noqa: BLE001 (the extrapolated sample stays the baseline)
+                    log(f"cpu_baseline_deterministic (same shape) failed: {ex}")
+                    line["cpu_baseline_deterministic"] = ext_det
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

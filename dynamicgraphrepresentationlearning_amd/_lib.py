@@ -22,7 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # WHARF_LIB_PATH: an alternative build of the same library (A/B experiments in tools/)
 LIB_PATH = os.environ.get("WHARF_LIB_PATH") or os.path.join(_HERE, "libwharf_gpu.so")
 
-ABI_VERSION = 7   # WHARF_ABI_VERSION of include/wharf_gpu.h
+ABI_VERSION = 8   # WHARF_ABI_VERSION of include/wharf_gpu.h
 WHARF_OK = 0
 WHARF_DEEPWALK, WHARF_NODE2VEC = 0, 1
 WHARF_INIT_RANDOM, WHARF_INIT_BURNIN, WHARF_INIT_WEIGHT = 0, 1, 2
@@ -70,6 +70,7 @@ class wharf_stats(C.Structure):
         ("last_anchor_inits", C.c_uint64),
         ("last_rewalk_passes", C.c_uint64),
         ("last_in_edge_mode", C.c_uint64),
+        ("rev_fallbacks", C.c_uint64),
     ]
 
 

@@ -885,8 +885,10 @@ void build_graph_from_keys(wharf_handle* h, uint64_t cnt, bool drop_loops, bool 
 {
     const uint64_t mm = h->unique_keys(cnt, drop_loops, 32 + std::max<uint32_t>(bits_for(h->n), 1));
     h->symmetric = symmetric_by_construction;
+    h->csr_from_keys(mm);   // (reads the keys, which stay for the symmetry check)
+    // the same rule as rev_wanted(): the slack-row pool's capacity, not the edge count
     const char* rv = getenv("WHARF_REV");
-    const bool rev_may = rv && *rv ? atoi(rv) != 0 : mm >= wharf_handle::kRevMinPool;
+    const bool rev_may = rv && *rv ? atoi(rv) != 0 : h->pool_cap >= wharf_handle::kRevMinPool;
     if (!symmetric_by_construction && (h->anchors || rev_may)) {   // (the anchor carry and the reverse index ask)
         unsigned long long* asym = h->errflag.as<unsigned long long>() + 3;
         HIPCHK(hipMemsetAsync(asym, 0, 8, h->s));
@@ -896,7 +898,6 @@ void build_graph_from_keys(wharf_handle* h, uint64_t cnt, bool drop_loops, bool 
         h->sync();
         h->symmetric = v == 0;
     }
-    h->csr_from_keys(mm);
     // the keys and sort temporaries are done with: free them before the records
     // (configs[4]: 2 x 29 GB of keys next to 131 GB of 32-B records)
     for (DevBuf* b : {&h->k1, &h->k2, &h->tmp, &h->flags}) b->release();
@@ -1279,24 +1280,27 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         h->dead_slots += dead;
         if (batch_asym) h->symmetric = false;
         if (h->rev_on && !h->symmetric) h->drop_rev();
-        // reverse-slot index: carried through the merge and used for the in-edge records
-        // unless a repack or compaction of this batch moved every row (then: scan, rebuild)
-        const bool use_rev = h->rev_on && h->rev_valid;
-        h->rev_pinned = use_rev;   // from here to the in-edge pass the index must stay (no reclaim)
-        if (use_rev) h->srev.ensure_grow(std::max<uint64_t>(saved, 1) * 4);
         // Anchor carry (node2vec MH on an undirected graph): the entries of the sources' rows travel
         // through the merge and only those whose anchor can change are reset (k_anchor_invalidate);
         // otherwise every entry of a rebuilt row starts empty.  WHARF_ANCHOR_CARRY=0 (A/B, tests).
         const char* acv = getenv("WHARF_ANCHOR_CARRY");
         const bool carry = h->anchors && h->symmetric && !(acv && *acv && atoi(acv) == 0);
         uint64_t* anc_base = h->anchors ? h->erec.as<uint64_t>() + 2 : nullptr;
+        // every per-batch buffer is allocated before the reverse index is pinned: an allocation that
+        // fails here can still reclaim the index (the batch then scans) instead of failing the batch
         if (carry) h->sanc.ensure_grow(std::max<uint64_t>(saved, 1) * 8);
-        h->grown = grow;
         h->scratch.ensure_grow(std::max<uint64_t>(saved, 1) * 4);
-        h->start_bound = saved + (insert ? total_chg : 0);   // the sources' degrees after the update, at most
-        const uint32_t rs = (uint32_t)h->rec_stride();
         // source rows in chunks: counts of each run's longest range, exclusive prefix (k_run_chunks)
         h->rchunk.ensure_grow((k + 1) * 8);
+        if (h->rev_on && h->rev_valid) h->srev.ensure_grow(std::max<uint64_t>(saved, 1) * 4);
+        // reverse-slot index: carried through the merge and used for the in-edge records
+        // unless a repack or compaction of this batch moved every row (then: scan, rebuild)
+        // or the allocations above reclaimed it
+        const bool use_rev = h->rev_on && h->rev_valid;
+        h->rev_pinned = use_rev;   // from here to the in-edge pass the index must stay (no reclaim)
+        h->grown = grow;
+        h->start_bound = saved + (insert ? total_chg : 0);   // the sources' degrees after the update, at most
+        const uint32_t rs = (uint32_t)h->rec_stride();
         uint32_t* rcnt = h->rchunk.as<uint32_t>();
         uint32_t* rpre = rcnt + (k + 1);
         launch_run_chunks(h->runs.as<RunInfo>(), h->rplan.as<RowPlan>(), k, rcnt, s);
@@ -1329,8 +1333,11 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             unsigned long long v = 0;
             HIPCHK(hipMemcpyAsync(&v, miss, 8, hipMemcpyDeviceToHost, s));
             h->sync();
-            if (v) {   // an edge without its reverse: cannot happen on a graph tracked as symmetric
+            if (v) {   // an edge without its reverse (1), or a stale carried entry (2, repaired before its
+                       // write): neither can happen on a graph tracked as symmetric.  The index is not
+                       // trusted again; the scan rewrites every in-edge record of the sources.
                 h->drop_rev();
+                h->st.rev_fallbacks++;
                 scan = true;
             }
         }

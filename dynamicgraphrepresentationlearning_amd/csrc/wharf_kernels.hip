@@ -211,6 +211,9 @@ __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp,
 #define WHARF_INIT_ROUNDS 2
 #endif
 constexpr uint32_t kInitRounds = WHARF_INIT_ROUNDS;   // proposals per active lane in flight
+#ifndef WHARF_RET_PRUNE
+#define WHARF_RET_PRUNE 0   // A/B (round 6): 1 = return pruning below; measured neutral, off by default
+#endif
 constexpr uint32_t kWavesPerBlock = 4;                // every walk kernel runs 256-thread blocks
 
 struct InitReq {     // a lane's init, published for the wave
@@ -252,6 +255,15 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
     // rank of each class by weight (ties share a rank, so the first proposal wins among them)
     const float w0 = a.inv_p, w1 = 1.0f, w2 = a.inv_q;
     const uint32_t rk0 = (w1 > w0) + (w2 > w0), rk1 = (w0 > w1) + (w2 > w1), rk2 = (w0 > w2) + (w1 > w2);
+    // Return pruning: when the return (1/p) is strictly the heaviest class, an init with a return
+    // among its proposals is settled by its first return whatever the others' classes, so once the
+    // targets are known the returns are published (key < 128: rank 0) and the other proposals of
+    // those inits read no filter word and probe no edge-hash bucket (exact; configs[4]'s p = .5,
+    // q = 2: ~24 % of the inits hold a return).  Measured neutral (round 6, profiles/r06/ret_prune:
+    // configs[4] first generation 1088-1098 vs 1094-1105 ms; the skipped filter words are lines of
+    // prev's own filter, mostly cache hits, and the 21 target loads bound the init), so it stays an
+    // A/B build (-DWHARF_RET_PRUNE=1, the GPU suite passed with it on).
+    const bool prune = WHARF_RET_PRUNE && rk0 == 0 && rk1 > 0 && rk2 > 0;
     const uint32_t total = cnt * kWeightProposals;
     for (uint32_t base = 0; base < total; base += nact * kInitRounds) {
         uint32_t t[kInitRounds], j[kInitRounds], cv[kInitRounds], fw[kInitRounds], fb[kInitRounds];
@@ -267,10 +279,22 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
                 cv[b] = a.adj[q.coff + pick32(r.x0, q.cdeg)];
             }
         }
+        bool settled[kInitRounds];   // this proposal's init has a return (prune): its class cannot win
+        if (prune) {
+#pragma unroll
+            for (uint32_t b = 0; b < kInitRounds; b++)
+                if (t[b] < cnt && cv[b] == s_req[wv][t[b]].pv) atomicMin(&s_key[wv][t[b]], j[b] << 2);
+            wave_lds_sync();
+#pragma unroll
+            for (uint32_t b = 0; b < kInitRounds; b++) settled[b] = t[b] < cnt && s_key[wv][t[b]] < 128u;
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < kInitRounds; b++) settled[b] = false;
+        }
 #pragma unroll
         for (uint32_t b = 0; b < kInitRounds; b++) {
             fw[b] = 0, fb[b] = 0;
-            if (t[b] < cnt && use_f && cv[b] != s_req[wv][t[b]].pv && !s_req[wv][t[b]].tonly) {
+            if (t[b] < cnt && use_f && cv[b] != s_req[wv][t[b]].pv && !s_req[wv][t[b]].tonly && !settled[b]) {
                 const uint64_t h = filt_hash(cv[b]);
                 fb[b] = filt_bits(h);
                 fw[b] = a.fpool[filt_word(s_req[wv][t[b]].fd, h)];
@@ -282,7 +306,8 @@ __device__ void anchor_init_wave(const WalkArgs& a, bool need, const Row& rc, co
             const InitReq q = s_req[wv][t[b]];
             uint32_t c;
             if (cv[b] == q.pv) c = 0;
-            else if (q.tonly) continue;        // only a return can settle a targets-only init
+            else if (q.tonly || settled[b]) continue;   // only a return can settle a targets-only init;
+                                                        // a return already settles this one
             else if (a.inv_q == 1.0f) c = 1;   // triangle and outward weigh the same
             else if (use_f && (fw[b] & fb[b]) != fb[b]) c = 2;   // filter negative: exact
             else c = has_edge(a, Row{q.pv, q.pdeg, 0u, q.poff}, cv[b]) ? 1 : 2;
@@ -3060,7 +3085,15 @@ __global__ void k_patch_rev(const RunInfo* __restrict__ runs, const uint32_t* __
             const Row ry = load_rec(erec, q * rs);   // the target y and its (new) row
             uint32_t x = ridx[q];
             // a source target's row was rebuilt (and so was its entry for s): search it; a new edge too
-            if (x == kNoRidx || ((bitmap[ry.v >> 5] >> (ry.v & 31)) & 1u)) {
+            bool search = x == kNoRidx || ((bitmap[ry.v >> 5] >> (ry.v & 31)) & 1u);
+            // a carried entry is checked before anything is written through it: outside y's row, or
+            // not at s, it is stale (an index bug) -- repaired by the search, and flagged so the host
+            // drops the index and the pool scan rewrites the records
+            if (!search && (x >= ry.deg || adj[ry.off + x] != s)) {
+                *miss = 2ull;
+                search = true;
+            }
+            if (search) {
                 const int64_t f = row_find(adj, ry, s);
                 if (f < 0) {
                     *miss = 1ull;

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define WHARF_ABI_VERSION 7
+#define WHARF_ABI_VERSION 8
 
 enum {
     WHARF_OK = 0,
@@ -94,6 +94,9 @@ typedef struct wharf_stats {
     uint64_t last_rewalk_passes;   /* node2vec MH re-walk by passes (k_rewalk_park): passes of the last update,
                                       0 when the lock-step kernel ran */
     uint64_t last_in_edge_mode;    /* 0: the last update scanned the pool for in-edges, 1: reverse-slot index */
+    uint64_t rev_fallbacks;        /* updates so far whose reverse-slot pass found an edge without its reverse or
+                                      a stale entry: the index was dropped and the pool scan rewrote the records
+                                      (0 on a healthy undirected stream; tests assert it) */
 } wharf_stats;
 
 typedef struct wharf_handle wharf_handle;

@@ -532,12 +532,22 @@ def test_reverse_slot_index(W, monkeypatch, rows, mode):
         e = O.generate_batch_of_edges(700, n, 60 + b, False, False)
         stream += [(True, e), (False, e)]
     stream.append((True, O.generate_batch_of_edges(900, n, 70, False, False)))
+    used = 0
     for ins, e in stream:
+        rp0 = g.stats()["repacks"]
         ga = (g.insert_edges_batch if ins else g.delete_edges_batch)(e, remove_dups=True)
         ra = ref.insert_edges_batch(e) if ins else ref.delete_edges_batch(e)
         assert np.array_equal(ga, ra)
         assert np.array_equal(g.walks(), ref.walks())
-        assert g.stats()["steps"] == ref.steps
+        st = g.stats()
+        assert st["steps"] == ref.steps
+        # the index served this batch's in-edge records unless the batch repacked or compacted the pool
+        # (every row moved: scan, then rebuild); it never missed (a miss drops it and scans)
+        assert st["rev_fallbacks"] == 0
+        assert st["last_in_edge_mode"] == (0 if st["repacks"] != rp0 else 1), (rows, st["repacks"], rp0)
+        used += st["last_in_edge_mode"]
+    if rows in ("slack", "slack-lazy"):   # rows merged in place: the index serves the batches
+        assert used >= len(stream) // 2
     o2, a2 = g.flatten_graph()
     o3, a3 = ref.csr()
     assert np.array_equal(o2, o3) and np.array_equal(a2, a3)
@@ -546,10 +556,12 @@ def test_reverse_slot_index(W, monkeypatch, rows, mode):
     d = O.generate_batch_of_edges(300, n, 80, False, True)
     assert np.array_equal(g.insert_edges_batch(d, remove_dups=True), ref.insert_edges_batch(d))
     assert np.array_equal(g.walks(), ref.walks())
+    assert g.stats()["last_in_edge_mode"] == 0
     assert g.memory_footprint(verbose=False)["csr_bytes"] <= held - 4 * g.number_of_edges()
     e = O.generate_batch_of_edges(500, n, 81, False, False)
     assert np.array_equal(g.insert_edges_batch(e, remove_dups=True), ref.insert_edges_batch(e))
     assert np.array_equal(g.walks(), ref.walks())
+    assert g.stats()["last_in_edge_mode"] == 0 and g.stats()["rev_fallbacks"] == 0
     g.destroy()
 
 

@@ -21,13 +21,19 @@ for rep in $(seq 1 $REPS); do
         ( [ -n "$envset" ] && export "$envset"; cd "$dir" && timeout -k 10 420 python -u bench.py $ARGS ) > "$log" 2>&1
         rc=$?
         echo "== $v rep $rep rc=$rc"
-        grep '^per_gpu_of_8 ' "$log" | \
-            python -c "
-import json,sys
-for l in sys.stdin:
-    if not l.startswith('per_gpu_of_8'): continue
-    k, j = l.split(': ', 1); d = json.loads(j)
-    print(k[13:], {x: d.get(x) for x in ('first_generation_ms', 'generation_ms', 'batch_median_ms', 'graph_update_median_ms', 'walk_update_median_ms', 'rewalk_kernel_median_ms', 'in_edge_records', 'device_bytes')})"
+        python - "$log" <<'PYEOF'
+import json, sys
+for l in open(sys.argv[1]):
+    if l.startswith('per_gpu_of_8 ') and ': {' in l:
+        k, j = l.split(': ', 1); d = json.loads(j)
+        print(k[13:], {x: d.get(x) for x in ('first_generation_ms', 'generation_ms', 'batch_median_ms', 'graph_update_median_ms', 'walk_update_median_ms', 'rewalk_kernel_median_ms', 'mean_anchor_inits', 'in_edge_records', 'device_bytes')})
+    elif l.startswith('{'):
+        d = json.loads(l)
+        n2v = d.get('mh_node2vec') or {}
+        rw = n2v.get('rewalk_latency_10k_batch') or {}
+        print('headline', d.get('value'), 'mh_node2vec first/warm gen ms', n2v.get('first_generation_kernel_ms'),
+              n2v.get('warm_generation_kernel_ms'), 'n2v rewalk median ms', rw.get('median_ms'))
+PYEOF
         [ $rc -eq 0 ] || exit $rc
     done
 done
