@@ -784,8 +784,8 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
     are agreed (minimum over the ranks) before anything is allocated, and every
     fallible local step is agreed before the next collective (distributed.agree),
     so a rank that fails makes every rank raise RankFailure instead of hanging."""
-    from dynamicgraphrepresentationlearning_amd.distributed import agree, agree_min, corpus_checksum, \
-        gather_corpus_chunked, injected_fault, local_corpus_checksum, shard_size
+    from dynamicgraphrepresentationlearning_amd.distributed import agree, agree_min, alloc_or_reclaim, \
+        corpus_checksum, gather_corpus_chunked, injected_fault, local_corpus_checksum, shard_size
     on_dev = comm_dev != "cpu"
     K_local = max(1, int(budget_bytes // (world * L * 4)))
     K = max(1, agree_min(K_local, device=comm_dev) if dist else K_local)
@@ -793,7 +793,8 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
     try:
         injected_fault("gather", rank)
         if not on_dev:
-            stage = torch.empty((K, L), dtype=torch.int32, device=f"cuda:{dev}")
+            stage = alloc_or_reclaim(lambda: torch.empty((K, L), dtype=torch.int32, device=f"cuda:{dev}"),
+                                     g.release_caches, rank)
     except Exception as ex:   # noqa: BLE001 (agreed: every rank abandons the gather)
         err = ex
     agree(err, "corpus gather setup", device=comm_dev)
@@ -810,7 +811,7 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
 
     barrier()
     t1 = time.perf_counter()
-    st = gather_corpus_chunked(read_local, shards, n, wpv, L, K, None, device=comm_dev)
+    st = gather_corpus_chunked(read_local, shards, n, wpv, L, K, None, device=comm_dev, on_oom=g.release_caches)
     barrier()
     ms = (time.perf_counter() - t1) * 1e3
     ms_all = _max_over_ranks(torch, dist, comm_dev, [ms])[0]
@@ -829,7 +830,7 @@ def corpus_gather_record(args, torch, dist, g, shards, n, wpv, L, dev, comm_dev,
             for r0, c, g0 in segs:
                 acc.add_(corpus_checksum(chunk[r0:r0 + c], g0, L))
 
-        gather_corpus_chunked(read_local, shards, n, wpv, L, K, sink, device=comm_dev)
+        gather_corpus_chunked(read_local, shards, n, wpv, L, K, sink, device=comm_dev, on_oom=g.release_caches)
         mine, err = None, None
         try:
             mine = local_corpus_checksum(read_local, shards[rank], n, wpv, L, K, device=comm_dev)

@@ -91,6 +91,7 @@ SIGNATURES = {
     "wharf_create_rmat": (_I, [_P, _U64, _U64, _U64, _U64, C.c_double, C.c_double, C.c_double, _I, _P]),
     "wharf_destroy": (_I, [_P]),
     "wharf_destroy_index": (_I, [_P]),
+    "wharf_release_caches": (_I, [_P, _P]),
     "wharf_generate": (_I, [_P]),
     "wharf_insert_edges": (_I, [_P, _U64, _P, _U32, _P, _P]),
     "wharf_delete_edges": (_I, [_P, _U64, _P, _U32, _P, _P]),

@@ -1497,6 +1497,16 @@ int wharf_destroy_index(wharf_handle* h)
     });
 }
 
+int wharf_release_caches(wharf_handle* h, uint64_t* freed_bytes)
+{
+    return guarded(h, [&] {
+        REQUIRE(h, WHARF_E_INVALID, "null handle");
+        const uint64_t held = h->rev.p ? (uint64_t)h->rev.cap + h->srev.cap : 0;
+        const bool dropped = h->reclaim();   // (not rebuilt lazily afterwards: the room is wanted elsewhere)
+        if (freed_bytes) *freed_bytes = dropped ? held : 0;
+    });
+}
+
 int wharf_generate(wharf_handle* h)
 {
     return guarded(h, [&] {

@@ -98,11 +98,39 @@ def agree_min(value: int, group=None, device="cpu") -> int:
 
 def injected_fault(phase: str, rank: int):
     """Test hook: WHARF_TEST_FAIL="<rank>:<phase>[,...]" makes that rank raise at
-    the start of that phase (tests/test_distributed_cpu.py drives a one-rank
-    failure through bench.py's jobs and the chunked gather)."""
+    that phase (tests/test_collective_safety.py drives a one-rank failure
+    through bench.py's jobs and the chunked gather).  A phase ending in "_oom"
+    raises torch.OutOfMemoryError, once per process."""
     spec = os.environ.get("WHARF_TEST_FAIL")
-    if spec and f"{rank}:{phase}" in spec.split(","):
+    key = f"{rank}:{phase}"
+    if spec and key in spec.split(",") and key not in _FIRED:
+        if phase.endswith("_oom"):
+            import torch
+            _FIRED.add(key)
+            raise torch.OutOfMemoryError(f"injected out of memory (WHARF_TEST_FAIL) at {phase} on rank {rank}")
         raise RuntimeError(f"injected fault (WHARF_TEST_FAIL) at {phase} on rank {rank}")
+
+
+_FIRED: set = set()
+
+
+def _is_oom(ex) -> bool:
+    import torch
+    return isinstance(ex, torch.OutOfMemoryError) or "out of memory" in str(ex).lower()
+
+
+def alloc_or_reclaim(alloc, on_oom, rank: int = 0):
+    """alloc(); if it runs out of device memory and on_oom is given (e.g.
+    WharfMH.release_caches: the library's reverse-slot index), free that and
+    try once more.  Local to the rank: the caller agrees the outcome."""
+    try:
+        injected_fault("alloc_oom", rank)
+        return alloc()
+    except Exception as ex:   # noqa: BLE001
+        if on_oom is None or not _is_oom(ex):
+            raise
+        on_oom()
+        return alloc()
 
 
 def balanced_shards(deg: np.ndarray, parts: int):
@@ -242,7 +270,7 @@ def shard_rows_to_global(shard, n: int, first: int, count: int):
 
 
 def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per_rank: int, sink=None,
-                          root: int | None = None, group=None, device="cpu", dtype=None):
+                          root: int | None = None, group=None, device="cpu", dtype=None, on_oom=None):
     """Bounded-memory corpus gather: all-gatherv (root None) or gatherv to `root`.
 
     shards: per rank, a (lo, hi) start-vertex range or a BlockShard;
@@ -257,8 +285,10 @@ def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per
     agreed before the first exchange, because chunk boundaries and receive
     sizes must be the same on every rank.  A failure on one rank (buffer,
     read_local, sink) is agreed before the next exchange and raises
-    RankFailure on every rank.  Returns {"chunks", "rows_per_rank",
-    "bytes_received", "bytes_sent"} of this rank.
+    RankFailure on every rank.  on_oom (e.g. WharfMH.release_caches): called
+    once when the chunk buffer does not fit, before one more try (the
+    library's droppable caches make room for it).  Returns {"chunks",
+    "rows_per_rank", "bytes_received", "bytes_sent"} of this rank.
     """
     import torch
     import torch.distributed as dist
@@ -274,7 +304,8 @@ def gather_corpus_chunked(read_local, shards, n: int, wpv: int, L: int, rows_per
     receives = root is None or rank == root
     buf, err = None, None
     try:
-        buf = torch.empty((K * (world if receives else 1), L), dtype=dtype, device=device)
+        buf = alloc_or_reclaim(lambda: torch.empty((K * (world if receives else 1), L), dtype=dtype, device=device),
+                               on_oom, rank)
     except Exception as ex:   # noqa: BLE001 (agreed below: every rank abandons the gather together)
         err = ex
     agree(err, "corpus gather buffer", group, device)

@@ -142,6 +142,13 @@ class WharfMH:
     def destroy_index(self) -> None:
         L.check(L.lib.wharf_destroy_index(self._h), self._h, "destroy_index")
 
+    def release_caches(self) -> int:
+        """Free the droppable device caches (the reverse-slot index) for an allocation of the
+        caller's that ran out of device memory; results are unchanged.  Returns the bytes freed."""
+        freed = C.c_uint64(0)
+        L.check(L.lib.wharf_release_caches(self._h, C.byref(freed)), self._h, "release_caches")
+        return int(freed.value)
+
     # -- queries ----------------------------------------------------------------------------
     def number_of_vertices(self) -> int:
         v = C.c_uint64()

@@ -127,6 +127,12 @@ int wharf_create_rmat(const wharf_config* cfg, uint64_t n, uint64_t edges_number
 int wharf_destroy(wharf_handle* h);
 /* WharfMH::destroy_index (wharfmh.h:237): drops every walk. */
 int wharf_destroy_index(wharf_handle* h);
+/* Frees the handle's droppable device caches -- the reverse-slot index (up to 4 B per pool slot,
+ * 16 GB at configs[4]) -- for a caller whose own allocation (e.g. a corpus gather buffer) ran out of
+ * device memory; the library does the same for its own failed allocations.  Results are unchanged
+ * (updates then scan the pool for in-edges); the index is not rebuilt lazily.  *freed_bytes (may be
+ * null) = bytes released, 0 when there was nothing to drop.  No reference counterpart. */
+int wharf_release_caches(wharf_handle* h, uint64_t* freed_bytes);
 
 /* WharfMH::generate_initial_random_walks (wharfmh.h:250-356). */
 int wharf_generate(wharf_handle* h);

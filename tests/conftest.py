@@ -6,6 +6,9 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
+# the reverse-slot index's carried entries are verified before each write in the test suite
+# (k_patch_rev<VERIFY>; a stale entry is repaired and counted in stats()["rev_fallbacks"])
+os.environ.setdefault("WHARF_REV_VERIFY", "1")
 
 
 def pytest_configure(config):

@@ -66,6 +66,12 @@ class FakeHandle:
 
     delete_edges_batch = insert_edges_batch
 
+    released = 0   # release_caches calls (class-wide: the tests read it after a job)
+
+    def release_caches(self):
+        FakeHandle.released += 1
+        return 0
+
     def destroy(self):
         pass
 

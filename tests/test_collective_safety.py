@@ -24,7 +24,8 @@ import torch.multiprocessing as mp
 WORLD = 2
 CASES = [("ok", "configs4", ""), ("build", "configs4", "1:build"), ("generation", "configs4", "1:generation"),
          ("gather", "configs4", "1:gather"), ("gather_read", "configs4", "0:gather_read"),
-         ("batch", "configs4", "1:batch"), ("one_gpu", "configs3", "1:one_gpu"), ("ok3", "configs3", "")]
+         ("batch", "configs4", "1:batch"), ("one_gpu", "configs3", "1:one_gpu"), ("ok3", "configs3", ""),
+         ("alloc_oom", "configs4", "1:alloc_oom")]
 
 
 def _free_port():
@@ -42,7 +43,7 @@ def _worker(rank, world, port, q):
     try:
         import torch
         import bench
-        from fake_wharf import FakeW, TorchProxy, walk_value
+        from fake_wharf import FakeHandle, FakeW, TorchProxy, walk_value
         from dynamicgraphrepresentationlearning_amd.distributed import block_shards, gather_corpus_chunked, \
             shard_size
         T = TorchProxy()
@@ -55,7 +56,9 @@ def _worker(rank, world, port, q):
         jobs = {}
         for tag, job, spec in CASES:
             os.environ["WHARF_TEST_FAIL"] = spec
+            FakeHandle.released = 0
             jobs[tag] = bench.multi_gpu_job(args, job, FakeW, T, 0, world, rank, dist, "cpu", barrier)
+            jobs[tag]["_released"] = FakeHandle.released
         os.environ.pop("WHARF_TEST_FAIL", None)
 
         # (a) unequal budgets: rank 0 can hold 3 rows per rank per chunk, rank 1 fifty
@@ -131,6 +134,12 @@ def test_one_rank_failure_is_agreed_by_every_rank(results, tag, job, spec):
             assert "one_gpu_same_graph" in recs[0]
         return
     bad_rank, phase = spec.split(":")
+    if phase == "alloc_oom":   # an out-of-memory buffer: the rank frees the library's caches and retries
+        for rank, r in enumerate(recs):
+            assert "error" not in r, r
+            assert r["corpus_allgatherv"]["checksum_of_checksums_ok"]
+            assert r["_released"] == (1 if rank == int(bad_rank) else 0), (rank, r["_released"])
+        return
     for r in recs:
         assert "error" in r, r
         assert r["failed_rank"] == int(bad_rank), r

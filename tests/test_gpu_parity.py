@@ -488,6 +488,47 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     _compare_stream(W, off, adj, batches, wpv=3, L=40, **kw)
 
 
+@pytest.mark.parametrize("mode", ["det", "node2vec"])
+def test_release_caches_drops_the_reverse_index(W, monkeypatch, mode):
+    """wharf_release_caches (a caller's allocation out of device memory, e.g. bench.py's gather
+    buffer): the reverse-slot index is freed (csr_bytes falls by >= 4 B per edge), later updates scan
+    the pool for in-edges, and the corpus, affected ids and CSR stay the oracle's; a second call
+    frees nothing."""
+    monkeypatch.setenv("WHARF_REV", "1")
+    n = 1 << 11
+    off, adj = O.csr_from_edges(n, O.generate_batch_of_edges(20000, 2 * n, 43, False, False))
+    kw = dict(deterministic=True) if mode == "det" else dict(
+        deterministic=False, seed=5, model=1, paramP=0.5, paramQ=2.0)
+    cfg = W.WharfConfig(walks_per_vertex=2, walk_length=24, **kw)
+    g = W.WharfMH.from_csr(off, adj, config=cfg)
+    ref = O.Engine(off, adj, wpv=2, L=24, model=cfg.model, p=cfg.paramP, q=cfg.paramQ, init=cfg.sampler_init,
+                   deterministic=cfg.deterministic, seed=cfg.seed)
+    g.generate_initial_random_walks()
+    ref.generate()
+    e = O.generate_batch_of_edges(300, n, 90, False, False)
+    assert np.array_equal(g.insert_edges_batch(e, remove_dups=True), ref.insert_edges_batch(e))
+    assert g.stats()["last_in_edge_mode"] == 1
+    held = g.memory_footprint(verbose=False)["csr_bytes"]
+    freed = g.release_caches()
+    assert freed >= 4 * g.number_of_edges()
+    assert g.memory_footprint(verbose=False)["csr_bytes"] <= held - 4 * g.number_of_edges()
+    assert g.release_caches() == 0
+    for ins in (False, True):
+        e = O.generate_batch_of_edges(300, n, 91, False, False)
+        ga = (g.insert_edges_batch if ins else g.delete_edges_batch)(e, remove_dups=True)
+        assert np.array_equal(ga, ref.insert_edges_batch(e) if ins else ref.delete_edges_batch(e))
+        assert np.array_equal(g.walks(), ref.walks())
+        assert g.stats()["last_in_edge_mode"] == 0 and g.stats()["rev_fallbacks"] == 0
+    g.generate_initial_random_walks()   # not rebuilt lazily after a release
+    ref.generate()
+    assert np.array_equal(g.walks(), ref.walks())
+    assert g.memory_footprint(verbose=False)["csr_bytes"] <= held - 4 * g.number_of_edges()
+    o2, a2 = g.flatten_graph()
+    o3, a3 = ref.csr()
+    assert np.array_equal(o2, o3) and np.array_equal(a2, a3)
+    g.destroy()
+
+
 @pytest.mark.parametrize("rows", ["slack", "slack-lazy", "move", "repack", "compact"])
 @pytest.mark.parametrize("mode", ["det", "deepwalk", "node2vec"])
 def test_reverse_slot_index(W, monkeypatch, rows, mode):
