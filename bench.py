@@ -151,7 +151,7 @@ def gather_ceiling(steps_per_s: float, live):
             "source": "tools/gather_roof 3.48 coarse dep, this box, before the timed region"}
 
 
-PMC_ROUNDS = ("r05_", "r04_", "r03_", "r02_", "")   # newest round's rocprofv3 summary first
+PMC_ROUNDS = ("r06_", "r05_", "r04_", "r03_", "r02_", "")   # newest round's rocprofv3 summary first
 
 
 def load_traffic(tag: str):
