@@ -453,3 +453,42 @@ def test_configs4_full_size_shard_of_8(W, torch):
         before = after
         doff = dadj = None
     g.destroy()
+
+
+def test_reverse_index_gate_follows_pool_capacity_for_csr_input(W, monkeypatch):
+    """a caller-supplied CSR (wharf_create, not symmetric by construction) whose edge
+    count is below the reverse index's 2^28-slot threshold while its slack-row pool is above it gets
+    the symmetry check, so the default index rule (pool capacity, rev_wanted) enables the index: the
+    first undirected batch's in-edge records go through it (last_in_edge_mode 1), and the CSR and the
+    affected ids equal those of a handle built with the index off."""
+    monkeypatch.delenv("WHARF_REV", raising=False)
+    n = 1 << 22
+    src = W.WharfMH.from_rmat(n, 131_000_000, 2 * n, seed=2, config=W.WharfConfig(walks_per_vertex=1, walk_length=8))
+    off, adj = src.flatten_graph()
+    src.destroy()
+    m = len(adj)
+    cfg = W.WharfConfig(walks_per_vertex=1, walk_length=8, model=W.DEEPWALK, deterministic=True)
+    g = W.WharfMH.from_csr(off, adj, config=cfg)
+    cap = g.stats()["pool_capacity"]
+    if not (m < (1 << 28) <= cap):
+        g.destroy()
+        pytest.skip(f"m={m}, pool capacity {cap}: not across the 2^28 threshold")
+    monkeypatch.setenv("WHARF_REV", "0")
+    h = W.WharfMH.from_csr(off, adj, config=cfg)
+    monkeypatch.delenv("WHARF_REV")
+    del off, adj
+    assert g.memory_footprint(verbose=False)["csr_bytes"] >= h.memory_footprint(verbose=False)["csr_bytes"] + 4 * m
+    g.generate_initial_random_walks()
+    h.generate_initial_random_walks()
+    e = W.generate_batch_of_edges(5000, n, 0, False, False)
+    ag = g.insert_edges_batch(e, remove_dups=True)
+    ah = h.insert_edges_batch(e, remove_dups=True)
+    assert g.stats()["last_in_edge_mode"] == 1 and g.stats()["rev_fallbacks"] == 0
+    assert h.stats()["last_in_edge_mode"] == 0
+    assert np.array_equal(ag, ah)
+    o1, a1 = g.flatten_graph()
+    o2, a2 = h.flatten_graph()
+    assert np.array_equal(o1, o2) and np.array_equal(a1, a2)
+    assert np.array_equal(g.walks(), h.walks())
+    g.destroy()
+    h.destroy()
