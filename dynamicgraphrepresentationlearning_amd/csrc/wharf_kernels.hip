@@ -780,60 +780,6 @@ __device__ __forceinline__ uint32_t start_vertex(const WalkArgs& a, uint64_t j)
     return (uint32_t)(a.lo + j);
 }
 
-#ifndef WHARF_NARROW_GEN
-#define WHARF_NARROW_GEN 0
-#endif
-#if WHARF_NARROW_GEN
-// A/B probe only (round 6; never the shipped build): the generation's stores in
-// a narrow walk matrix.  Every lane steps to L - 1 (a dead lane stores kSent), and
-// WHARF_NARROW_GEN=1 packs four 24-bit ids of lanes 4q..4q+3 into three dwords (lane k < 3 stores
-// dword k, its neighbour's id by one shuffle): 3 B per position instead of 4.  =2 keeps the same loop
-// with 4-B stores (the loop change alone).  Nothing else reads this layout: bench's headline only.
-template <int MODEL, bool DET, bool BLK = false>
-__global__ __launch_bounds__(256) void k_walk(WalkArgs a)
-{
-    uint32_t steps = 0, accepts = 0, inits = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint32_t* __restrict__ walks = a.walks;
-    const uint64_t W = a.W, Wd = a.W / 4 * 3;
-    for (uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; li < W; li += stride) {
-        const uint64_t r = li / a.n_loc;
-        const uint32_t v = start_vertex<BLK>(a, li - r * a.n_loc);
-        const uint64_t wid = r * a.n + v;
-        const uint32_t ep = a.epoch << 4, wlo = (uint32_t)wid, whi = (uint32_t)(wid >> 32);
-        const uint64_t* __restrict__ rt = DET ? a.rtab + r * a.L : nullptr;
-        const uint32_t k = (uint32_t)(li & 3u);
-        const uint64_t q3 = (li >> 2) * 3;
-        auto put = [&](uint32_t pos, uint32_t x) {
-            if constexpr (WHARF_NARROW_GEN == 1) {
-                const uint32_t nx = __shfl_down(x, 1, 4);
-                const uint32_t d = k == 0 ? ((x & 0xFFFFFFu) | (nx << 24))
-                                 : k == 1 ? (((x >> 8) & 0xFFFFu) | (nx << 16))
-                                          : (((x >> 16) & 0xFFu) | (nx << 8));
-                if (k < 3) walks[(uint64_t)pos * Wd + q3 + k] = d;
-            } else {
-                walks[(uint64_t)pos * W + li] = x;
-            }
-        };
-        put(0, v);
-        Walker w;
-        walk_state<MODEL, DET>(a, v, v, 0, wlo, whi, ep, w);
-        bool alive = true;
-        for (uint32_t pos = 0; pos + 1 < a.L; pos++) {
-            alive = alive && w.rc.deg != 0;   // dead end: the walk stops (reference: lrand() % 0)
-            uint32_t x = kSent;
-            if (alive) {
-                x = walk_step<MODEL, DET>(a, w, rt, pos, wlo, whi, ep, accepts, inits);
-                steps++;
-            }
-            put(pos + 1, x);
-        }
-    }
-    wave_add(a.counters + 0, steps);
-    wave_add(a.counters + 1, accepts);
-    wave_add(a.counters + 7, inits);
-}
-#else
 template <int MODEL, bool DET, bool BLK = false>
 __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
 {
@@ -862,7 +808,6 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
     wave_add(a.counters + 1, accepts);
     wave_add(a.counters + 7, inits);
 }
-#endif
 
 // Fused rewalk-point scan + suffix re-walk (wharfmh.h:519-537 + 761-859),
 // DeepWalk and deterministic mode.  The rewalk point of a walk is the first
