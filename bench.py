@@ -1246,6 +1246,11 @@ def main():
                          "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src,
+                         # the PMC bytes per launch moved in this run's average launch time: how close the
+                         # random line fetches run to the HBM peak (frac is by algorithmic bytes)
+                         "traffic_GBps": round(traffic / (avg_kernel_ms * 1e-3) / 1e9, 1) if traffic else None,
+                         "traffic_frac_of_peak": round(traffic / (avg_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                         if traffic else None,
                          "bytes_per_step": bytes_per_step,
                          "avg_kernel_ms": round(avg_kernel_ms, 3),
                          # the first generation of a fresh handle (node2vec: every anchor initialised)
