@@ -409,7 +409,7 @@ struct wharf_handle {
     void make_room(uint64_t extra)
     {
         const uint64_t pc = pool_capacity(pool_used, extra);
-        const uint64_t need = pc * (4 + sizeof(ERec) * rec_stride()) + 3 * (n + 1) * 8 + (256ull << 20);
+        const uint64_t need = pc * 4 + rec_bytes(rec_fmt_for(pc), pc, rec_stride()) + 3 * (n + 1) * 8 + (256ull << 20);
         if (need <= free_bytes()) {
             try {
                 repack(extra);
@@ -444,7 +444,7 @@ struct wharf_handle {
             const uint64_t pc = pool_capacity(used, extra);
             adj2.ensure(std::max<uint64_t>(pc, 1) * 4);
             HIPCHK(hipMemsetAsync(adj2.p, 0xFF, std::max<uint64_t>(pc, 1) * 4, s));
-            erec2.ensure(std::max<uint64_t>(pc, 1) * sizeof(ERec) * rs);
+            erec2.ensure(rec_bytes(rec_fmt_for(pc), pc, rs));   // (the records are rebuilt below)
             launch_copy_rows(off.as<uint64_t>(), deg.as<uint32_t>(), adj.as<uint32_t>(), off2.as<uint64_t>(), n,
                              adj2.as<uint32_t>(), anchors ? erec.as<uint64_t>() + 2 : nullptr,
                              anchors ? erec2.as<uint64_t>() + 2 : nullptr, s);
@@ -456,6 +456,7 @@ struct wharf_handle {
             std::swap(cap, cap2);
             pool_used = used;
             pool_cap = pc;
+            rf = rec_fmt_for(pc);
         } catch (...) {
             capw.release();
             cap2.release();
@@ -470,7 +471,7 @@ struct wharf_handle {
         erec2.release();
         dead_slots = 0;
         launch_vrec(off.as<uint64_t>(), deg.as<uint32_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
-        launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rs, 1, s);
+        launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rs, 1, rf, s);
         repacks++;
         rev_valid = false;   // every row moved: the reverse-slot index is rebuilt after the batch
     }
@@ -537,7 +538,7 @@ struct wharf_handle {
         for (DevBuf* b : {&order, &snoff, &sadj, &sanc}) b->release();
         dead_slots = 0;
         launch_vrec(off.as<uint64_t>(), deg.as<uint32_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
-        launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rs, 1, s);
+        launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rs, 1, rf, s);
         repacks++;
         rev_valid = false;   // every row moved: the reverse-slot index is rebuilt after the batch
     }
@@ -633,15 +634,40 @@ struct wharf_handle {
     // 16-B edge records, 32 B with the anchor entry (node2vec MH)
     uint64_t rec_stride() const { return anchors ? 2 : 1; }
 
+    // The edge-record layout for a pool of pc slots: compact 8-B records (wharf_device.h RecFmt)
+    // for a handle without anchors whose vertex ids and slot offsets leave at least
+    // kMinCompactDegBits for the degree, else the 16-B layout.  WHARF_COMPACT_REC=0 (A/B, tests)
+    // keeps the 16-B layout.
+    RecFmt rf{0u, 0u, 0u};
+    RecFmt rec_fmt_for(uint64_t pc) const
+    {
+        const char* e = getenv("WHARF_COMPACT_REC");
+        if (anchors || (e && *e && atoi(e) == 0)) return RecFmt{0u, 0u, 0u};
+        const uint32_t vb = std::max<uint32_t>(bits_for(std::max<uint64_t>(n, 2)), 1);
+        uint32_t ob = std::max<uint32_t>(bits_for(std::max<uint64_t>(pc, 2)), 1);
+        if (vb + ob + kMinCompactDegBits > 64) return RecFmt{0u, 0u, 0u};
+        const char* db = getenv("WHARF_COMPACT_DEG_BITS");   // tests: a narrow degree field, so rows of
+        if (db && *db) {                                     // degree >= 2^db - 1 take the escape
+            const uint32_t d = std::min<uint32_t>(std::max<int>(atoi(db), 1), 32);
+            if (vb + ob + d <= 64) ob = 64 - vb - d;
+        }
+        return RecFmt{1u, vb, ob};
+    }
+    static uint64_t rec_bytes(RecFmt f, uint64_t slots, uint64_t rs)
+    {
+        return std::max<uint64_t>(slots, 1) * (f.compact ? 8 : sizeof(ERec) * rs);
+    }
+
     // vertex rows and per-slot edge records (one gather per walk step);
     // anchor entries start empty
     void build_records()
     {
         vrec.ensure(std::max<uint64_t>(n, 1) * sizeof(ERec));
         erec.release();
-        erec.ensure(std::max<uint64_t>(pool_cap, 1) * sizeof(ERec) * rec_stride());
+        rf = rec_fmt_for(pool_cap);
+        erec.ensure(rec_bytes(rf, pool_cap, rec_stride()));
         launch_vrec(off.as<uint64_t>(), deg.as<uint32_t>(), n, row_epoch.as<uint32_t>(), vrec.as<ERec>(), s);
-        launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rec_stride(), 0, s);
+        launch_erec(adj.as<uint32_t>(), pool_used, vrec.as<ERec>(), erec.as<ERec>(), (uint32_t)rec_stride(), 0, rf, s);
     }
 
     void build_edge_hash()
@@ -717,6 +743,8 @@ struct wharf_handle {
         WalkArgs a{};
         a.vrec = vrec.as<ERec>();
         a.erec = erec.as<ERec>();
+        a.rf = rf;
+        a.deg = deg.as<uint32_t>();
         a.adj = adj.as<uint32_t>();
         a.anchor = anchors ? erec.as<uint64_t>() + 2 : nullptr;   // inside the 32-B records
         a.ehash = anchors ? ehash.as<uint64_t>() : nullptr;
@@ -1321,7 +1349,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         // records: the source rows' slots (anchors reset), then every slot whose
         // target is a source (one streaming scan of the pool)
         launch_erec_rows(h->runs.as<RunInfo>(), k, rpre, h->off.as<uint64_t>(), h->deg.as<uint32_t>(), h->adj.as<uint32_t>(),
-                         h->vrec.as<ERec>(), h->erec.as<ERec>(), rs, carry ? 1 : 0, s);
+                         h->vrec.as<ERec>(), h->erec.as<ERec>(), rs, carry ? 1 : 0, h->rf, s);
         HIPCHK(hipEventRecord(h->ev[4], s));
         bool scan = !use_rev;
         if (use_rev) {   // the sources' in-edges from their own rows (k_patch_rev)
@@ -1329,7 +1357,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
             HIPCHK(hipMemsetAsync(miss, 0, 8, s));
             launch_patch_rev(h->runs.as<RunInfo>(), k, rpre, h->off.as<uint64_t>(), h->deg.as<uint32_t>(),
                              h->adj.as<uint32_t>(), h->bitmap.as<uint32_t>(), h->vrec.as<ERec>(), h->erec.as<ERec>(), rs,
-                             h->rev.as<uint32_t>(), miss, s);
+                             h->rf, h->rev.as<uint32_t>(), miss, s);
             unsigned long long v = 0;
             HIPCHK(hipMemcpyAsync(&v, miss, 8, hipMemcpyDeviceToHost, s));
             h->sync();
@@ -1344,7 +1372,7 @@ int do_update(wharf_handle* h, bool insert, uint64_t m, const uint32_t* pairs, u
         if (scan)
             launch_patch_in_edges(h->adj.as<uint32_t>(), h->pool_used, h->bitmap.as<uint32_t>(),
                                   h->bitmap.as<uint32_t>() + h->bitmap_words(), h->vrec.as<ERec>(), h->erec.as<ERec>(),
-                                  rs, s);
+                                  rs, h->rf, s);
         HIPCHK(hipEventRecord(h->ev[5], s));
         h->rev_pinned = false;
         if (h->rev_on && !h->rev_valid) h->build_rev();   // after a repack / compaction in this batch
@@ -2122,7 +2150,8 @@ int wharf_get_stats(const wharf_handle* h, wharf_stats* out)
     out->m = h->m;
     out->walks = h->W;
     out->hbm_bytes_walks = h->W * h->L * 4;
-    out->hbm_bytes_graph = (h->n + 1) * 8 + h->n * 8 + h->pool_cap * 4 + (h->n + h->pool_cap * h->rec_stride()) * sizeof(ERec);
+    out->hbm_bytes_graph = (h->n + 1) * 8 + h->n * 8 + h->pool_cap * 4 + h->n * sizeof(ERec) +
+                           wharf_handle::rec_bytes(h->rf, h->pool_cap, h->rec_stride());
     out->pool_slots = h->pool_used;
     out->pool_capacity = h->pool_cap;
     out->last_moved_row_slots = h->grown;

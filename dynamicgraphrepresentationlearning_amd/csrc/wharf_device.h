@@ -141,6 +141,55 @@ __device__ __forceinline__ Row load_rec(const ERec* p, uint64_t i)
     return r;
 }
 
+// Compact 8-B edge records (round 6).  A DeepWalk or deterministic handle needs no
+// row epoch in its edge records (only node2vec MH anchors read it), and when its
+// vertex ids and pool offsets leave enough bits, a slot's record packs into one
+// u64: v | off << vb | deg << (vb + ob).  A degree of 2^db - 1 or more (db = 64 -
+// vb - ob) is stored as the escape 2^db - 1 and read from deg[v] (RMAT hubs: at
+// configs[1], db = 14 and ~2 % of steps land on an escaped row).  Half the bytes
+// per slot halve the table the walk's random gathers land in, and more of it stays
+// in L2 and the Infinity Cache (tools/gather_roof: a 1.74-GiB table gathers ~10 %
+// faster than 3.48 GiB).  compact = 0: the 16-B ERec layout.
+struct RecFmt {
+    uint32_t compact, vb, ob;
+};
+constexpr uint32_t kMinCompactDegBits = 12;
+
+__host__ __device__ __forceinline__ uint64_t pack_rec8(const ERec& r, RecFmt f)
+{
+    const uint32_t db = 64 - f.vb - f.ob;
+    const uint64_t dmax = (db >= 32 ? 0xFFFFFFFFull : ((1ull << db) - 1));
+    const uint64_t d = r.deg < dmax ? r.deg : dmax;
+    return (uint64_t)r.v | ((r.oe & kOffMask) << f.vb) | (d << (f.vb + f.ob));
+}
+
+__device__ __forceinline__ Row unpack_rec8(uint64_t q, RecFmt f, const uint32_t* __restrict__ deg)
+{
+    const uint32_t db = 64 - f.vb - f.ob;
+    const uint64_t dmax = (db >= 32 ? 0xFFFFFFFFull : ((1ull << db) - 1));
+    Row r;
+    r.v = (uint32_t)(q & ((1ull << f.vb) - 1));
+    r.off = (q >> f.vb) & ((1ull << f.ob) - 1);
+    const uint64_t d = q >> (f.vb + f.ob);
+    r.deg = d == dmax ? deg[r.v] : (uint32_t)d;   // the escape: a hub's degree from its row
+    r.epoch = 0;
+    return r;
+}
+
+// slot e's record in either layout (rs: 16-B units per slot of the 16-B layout)
+__device__ __forceinline__ Row load_erec(const ERec* __restrict__ erec, uint64_t e, uint32_t rs, RecFmt f,
+                                         const uint32_t* __restrict__ deg)
+{
+    if (f.compact) return unpack_rec8(reinterpret_cast<const uint64_t*>(erec)[e], f, deg);
+    return load_rec(erec, e * rs);
+}
+
+__device__ __forceinline__ void store_erec(ERec* __restrict__ erec, uint64_t e, uint32_t rs, const ERec& r, RecFmt f)
+{
+    if (f.compact) reinterpret_cast<uint64_t*>(erec)[e] = pack_rec8(r, f);
+    else erec[e * rs] = r;
+}
+
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (Random123); 10 rounds, key bumped between rounds.
 // ---------------------------------------------------------------------------

@@ -22,7 +22,9 @@ struct RunInfo {
 
 struct WalkArgs {
     const ERec* vrec;            // [n]: the row of each vertex
-    const ERec* erec;            // [m]: per CSR slot, the target's row
+    const ERec* erec;            // [m]: per CSR slot, the target's row (16 B, 32 B with the anchor, or 8 B: rf)
+    RecFmt rf;                   // edge-record layout (compact 8-B records: DeepWalk / deterministic)
+    const uint32_t* deg;         // [n]: row degrees (a compact record's degree escape)
     const uint32_t* adj;         // [m]: CSR targets (binary searches, anchor proposals)
     uint64_t* anchor;            // node2vec MH: anchor entry of CSR slot e at anchor[e * kAnchorStride]
                                  //   (bytes 16-23 of the slot's 32-B edge record)
@@ -103,7 +105,7 @@ void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t s
 void launch_vrec(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* row_epoch, ERec* vrec,
                  hipStream_t s);
 void launch_erec(const uint32_t* adj, uint64_t slots, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anchors,
-                 hipStream_t s);
+                 RecFmt rf, hipStream_t s);
 void launch_rmat_keys(const RmatParams& p, uint64_t M, int directed, uint64_t* keys, hipStream_t s);
 void launch_pairs_to_keys(const uint32_t* pairs, uint64_t m, uint64_t n, uint64_t* keys, unsigned long long* err, hipStream_t s);
 void launch_csr_to_keys(const uint64_t* off, uint64_t n, const uint32_t* tgt, uint64_t* keys, unsigned long long* err, hipStream_t s);
@@ -151,16 +153,17 @@ void launch_keys_symmetric(const uint64_t* keys, uint64_t m, unsigned long long*
 void launch_commit_rows(const RunInfo* runs, uint64_t k, const RowPlan* plan, uint32_t epoch, uint64_t* off,
                         uint32_t* deg, uint32_t* cap, ERec* vrec, uint32_t* row_epoch, hipStream_t s);
 void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* off, const uint32_t* deg,
-                      const uint32_t* adj, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anc, hipStream_t s);
+                      const uint32_t* adj, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anc, RecFmt rf,
+                      hipStream_t s);
 void launch_patch_in_edges(const uint32_t* adj, uint64_t slots, const uint32_t* bitmap, const uint32_t* bloom,
-                           const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s);
+                           const ERec* vrec, ERec* erec, uint32_t rs, RecFmt rf, hipStream_t s);
 // reverse-slot index (undirected graphs): ridx[e] = the index of x in y's row for slot e = (x -> y)
 constexpr uint32_t kNoRidx = 0xFFFFFFFFu;
 void launch_rev_build(const uint64_t* off, const uint32_t* deg, const uint32_t* adj, uint64_t n, uint64_t slots,
                       uint32_t* ridx, unsigned long long* miss, hipStream_t s);
 void launch_patch_rev(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* off, const uint32_t* deg,
                       const uint32_t* adj, const uint32_t* bitmap, const ERec* vrec, ERec* erec, uint32_t rs,
-                      uint32_t* ridx, unsigned long long* miss, hipStream_t s);
+                      RecFmt rf, uint32_t* ridx, unsigned long long* miss, hipStream_t s);
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s);
 void launch_gather_rows(const uint32_t* walks, uint64_t W, uint32_t L, const uint64_t* list, uint64_t base,
                         uint64_t count, uint32_t* out, hipStream_t s);

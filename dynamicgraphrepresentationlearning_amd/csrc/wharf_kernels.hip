@@ -413,9 +413,13 @@ struct Walker {
 template <int MODEL, bool DET>
 __device__ __forceinline__ Row load_edge(const WalkArgs& a, uint64_t e, uint64_t& anc)
 {
-    const Row r = load_rec(a.erec, e * kRecStride<MODEL, DET>);
-    if constexpr (kRecStride<MODEL, DET> == 2) anc = a.anchor[e * kAnchorStride];   // same 32-B record
-    return r;
+    if constexpr (kRecStride<MODEL, DET> == 2) {
+        const Row r = load_rec(a.erec, e * 2);
+        anc = a.anchor[e * kAnchorStride];   // same 32-B record
+        return r;
+    } else {
+        return load_erec(a.erec, e, 1, a.rf, a.deg);   // 16 B, or 8 B (compact)
+    }
 }
 
 // One transition cur -> next from position `pos` (deepwalk.h:64-87 /
@@ -434,7 +438,7 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
     Row nx;
     if constexpr (DET) {
         // rt = Random(wid / n) restarted at the walk's first re-walked position
-        nx = load_rec(a.erec, w.rc.off + umod64_32(rt[pos], w.rc.deg));
+        nx = load_erec(a.erec, w.rc.off + umod64_32(rt[pos], w.rc.deg), 1, a.rf, a.deg);
     } else {
         const P4 q = philox4x32_10(wlo, whi, pos, ep | kStreamStep, a.key0, a.key1);
         const uint32_t ci = (uint32_t)pick32(q.x0, w.rc.deg);
@@ -2370,12 +2374,12 @@ __global__ void k_vrec(const uint64_t* __restrict__ off, const uint32_t* __restr
 // its target's row (rs = 2: 32-B records whose anchor entry starts empty,
 // unless keep_anchors: a repack copied them along)
 __global__ void k_erec(const uint32_t* __restrict__ adj, uint64_t slots, const ERec* __restrict__ vrec,
-                       ERec* __restrict__ erec, uint32_t rs, int keep_anchors)
+                       ERec* __restrict__ erec, uint32_t rs, int keep_anchors, RecFmt rf)
 {
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t t = adj[e];
         if (t == kGap) continue;
-        erec[e * rs] = vrec[t];
+        store_erec(erec, e, rs, vrec[t], rf);
         if (rs == 2 && !keep_anchors) reinterpret_cast<uint64_t*>(erec)[e * kAnchorStride + 2] = kAnchorNone64;
     }
 }
@@ -2387,9 +2391,10 @@ void launch_vrec(const uint64_t* off, const uint32_t* deg, uint64_t n, const uin
 }
 
 void launch_erec(const uint32_t* adj, uint64_t slots, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anchors,
-                 hipStream_t s)
+                 RecFmt rf, hipStream_t s)
 {
-    if (slots) hipLaunchKernelGGL(k_erec, grid_for(slots, 256), 256, 0, s, adj, slots, vrec, erec, rs, keep_anchors);
+    if (slots)
+        hipLaunchKernelGGL(k_erec, grid_for(slots, 256), 256, 0, s, adj, slots, vrec, erec, rs, keep_anchors, rf);
 }
 
 // Per batch edge (sorted, unique): does it change its source row?
@@ -2767,7 +2772,7 @@ __global__ void k_resolve_plan(const RunInfo* __restrict__ runs, uint64_t k, con
 __global__ void k_erec_rows_c(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
                               const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg,
                               const uint32_t* __restrict__ adj, const ERec* __restrict__ vrec, ERec* __restrict__ erec,
-                              uint32_t rs, int keep_anc)
+                              uint32_t rs, int keep_anc, RecFmt rf)
 {
     for (uint64_t t = blockIdx.x;; t += gridDim.x) {   // chunk t: run j's chunk c, slots [lo, lo + kRowChunk)
         uint64_t j;
@@ -2777,7 +2782,7 @@ __global__ void k_erec_rows_c(const RunInfo* __restrict__ runs, const uint32_t* 
         const uint32_t s = runs[j].src;
         const uint64_t b = off[s], e = b + deg[s];
         for (uint64_t q = b + lo + threadIdx.x; q < min(e, b + lo + kRowChunk); q += blockDim.x) {
-            erec[q * rs] = vrec[adj[q]];
+            store_erec(erec, q, rs, vrec[adj[q]], rf);
             if (rs == 2 && !keep_anc) reinterpret_cast<uint64_t*>(erec)[q * kAnchorStride + 2] = kAnchorNone64;
         }
     }
@@ -2850,12 +2855,13 @@ __global__ void k_commit_rows(const RunInfo* __restrict__ runs, uint64_t k, cons
 // source's row) start empty: see anchor_lookup and DESIGN.md §4
 __global__ void k_erec_rows(const RunInfo* __restrict__ runs, const uint64_t* __restrict__ off,
                             const uint32_t* __restrict__ deg, const uint32_t* __restrict__ adj,
-                            const ERec* __restrict__ vrec, ERec* __restrict__ erec, uint32_t rs, int keep_anc)
+                            const ERec* __restrict__ vrec, ERec* __restrict__ erec, uint32_t rs, int keep_anc,
+                            RecFmt rf)
 {
     const uint32_t s = runs[blockIdx.x].src;
     const uint64_t b = off[s], e = b + deg[s];
     for (uint64_t j = b + threadIdx.x; j < e; j += blockDim.x) {
-        erec[j * rs] = vrec[adj[j]];
+        store_erec(erec, j, rs, vrec[adj[j]], rf);
         if (rs == 2 && !keep_anc) reinterpret_cast<uint64_t*>(erec)[j * kAnchorStride + 2] = kAnchorNone64;
     }
 }
@@ -2934,9 +2940,9 @@ __global__ void k_keys_symmetric(const uint64_t* __restrict__ keys, uint64_t m, 
 // the pool's targets, four slots per 16-B load; the Bloom filter of the
 // sources sits in LDS and only its positives read the exact bitmap.
 __device__ __forceinline__ void patch_slot(uint32_t t, uint64_t e, const uint32_t* bitmap, const ERec* vrec, ERec* erec,
-                                           uint32_t rs)
+                                           uint32_t rs, RecFmt rf)
 {
-    if (t != kGap && ((bitmap[t >> 5] >> (t & 31)) & 1u)) erec[e * rs] = vrec[t];
+    if (t != kGap && ((bitmap[t >> 5] >> (t & 31)) & 1u)) store_erec(erec, e, rs, vrec[t], rf);
 }
 
 // 1024-thread workgroups, two per CU (the 64-KiB filter in LDS), 32 waves per CU (8 per SIMD: 64 VGPRs)
@@ -2956,7 +2962,7 @@ __global__ __launch_bounds__(1024, 8) void k_patch_in_edges(const uint32_t* __re
                                                         const uint32_t* __restrict__ bitmap,
                                                         const uint32_t* __restrict__ bloom_big,
                                                         const ERec* __restrict__ vrec, ERec* __restrict__ erec,
-                                                        uint32_t rs)
+                                                        uint32_t rs, RecFmt rf)
 {
     __shared__ uint32_t s_bloom[kBigBloomWords];
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -2996,13 +3002,13 @@ __global__ __launch_bounds__(1024, 8) void k_patch_in_edges(const uint32_t* __re
         if (!__any(hits != 0)) continue;
         for (uint32_t m = hits; m; m &= m - 1u) {
             const uint32_t b = (uint32_t)__builtin_ctz(m);
-            patch_slot(tv[b >> 2][b & 3u], 4 * (uint64_t)(q0 + (b >> 2) * stride) + (b & 3u), bitmap, vrec, erec, rs);
+            patch_slot(tv[b >> 2][b & 3u], 4 * (uint64_t)(q0 + (b >> 2) * stride) + (b & 3u), bitmap, vrec, erec, rs, rf);
         }
     }
     if (g < slots - 4 * (uint64_t)n4) {   // the pool's last < 4 slots
         const uint64_t e = 4 * (uint64_t)n4 + g;
         const uint32_t x = adj[e];
-        if (bloom_test_big(s_bloom, x)) patch_slot(x, e, bitmap, vrec, erec, rs);
+        if (bloom_test_big(s_bloom, x)) patch_slot(x, e, bitmap, vrec, erec, rs, rf);
     }
 }
 
@@ -3069,7 +3075,7 @@ template <bool VERIFY>
 __global__ void k_patch_rev(const RunInfo* __restrict__ runs, const uint32_t* __restrict__ pre, uint64_t k,
                             const uint64_t* __restrict__ off, const uint32_t* __restrict__ deg,
                             const uint32_t* __restrict__ adj, const uint32_t* __restrict__ bitmap,
-                            const ERec* __restrict__ vrec, ERec* __restrict__ erec, uint32_t rs,
+                            const ERec* __restrict__ vrec, ERec* __restrict__ erec, uint32_t rs, RecFmt rf,
                             uint32_t* __restrict__ ridx, unsigned long long* __restrict__ miss)
 {
     // (pieces of 256 slots — one per thread — instead of the 4096-slot chunks were slower: the
@@ -3083,7 +3089,7 @@ __global__ void k_patch_rev(const RunInfo* __restrict__ runs, const uint32_t* __
         const uint64_t b = off[s], e = b + deg[s];
         const ERec rec = vrec[s];
         for (uint64_t q = b + lo + threadIdx.x; q < min(e, b + lo + kRowChunk); q += blockDim.x) {
-            const Row ry = load_rec(erec, q * rs);   // the target y and its (new) row
+            const Row ry = load_erec(erec, q, rs, rf, deg);   // the target y and its (new) row
             uint32_t x = ridx[q];
             // a source target's row was rebuilt (and so was its entry for s): search it; a new edge too
             bool search = x == kNoRidx || ((bitmap[ry.v >> 5] >> (ry.v & 31)) & 1u);
@@ -3105,7 +3111,7 @@ __global__ void k_patch_rev(const RunInfo* __restrict__ runs, const uint32_t* __
                 ridx[q] = x;
             }
             const uint64_t r = ry.off + x;
-            erec[r * rs] = rec;   // the 16-B row part (node2vec: the anchor entry behind it stays)
+            store_erec(erec, r, rs, rec, rf);   // the row part (node2vec: the anchor entry behind it stays)
             ridx[r] = (uint32_t)(q - b);
         }
     }
@@ -3120,7 +3126,7 @@ void launch_rev_build(const uint64_t* off, const uint32_t* deg, const uint32_t* 
 
 void launch_patch_rev(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* off, const uint32_t* deg,
                       const uint32_t* adj, const uint32_t* bitmap, const ERec* vrec, ERec* erec, uint32_t rs,
-                      uint32_t* ridx, unsigned long long* miss, hipStream_t s)
+                      RecFmt rf, uint32_t* ridx, unsigned long long* miss, hipStream_t s)
 {
     // workgroups per CU (each deals 4096-slot chunks of the sources' rows; A/B: WHARF_PATCH_REV_WG)
     static const int per_cu = [] {
@@ -3134,10 +3140,10 @@ void launch_patch_rev(const RunInfo* runs, uint64_t k, const uint32_t* pre, cons
     if (k) {
         if (verify)
             hipLaunchKernelGGL(k_patch_rev<true>, cu_count() * per_cu, 256, 0, s, runs, pre, k, off, deg, adj, bitmap,
-                               vrec, erec, rs, ridx, miss);
+                               vrec, erec, rs, rf, ridx, miss);
         else
             hipLaunchKernelGGL(k_patch_rev<false>, cu_count() * per_cu, 256, 0, s, runs, pre, k, off, deg, adj, bitmap,
-                               vrec, erec, rs, ridx, miss);
+                               vrec, erec, rs, rf, ridx, miss);
     }
 }
 
@@ -3520,13 +3526,15 @@ void launch_commit_rows(const RunInfo* runs, uint64_t k, const RowPlan* plan, ui
                         uint32_t* deg, uint32_t* cap, ERec* vrec, uint32_t* row_epoch, hipStream_t s)
 { if (k) hipLaunchKernelGGL(k_commit_rows, grid_for(k, 256), 256, 0, s, runs, k, plan, epoch, off, deg, cap, vrec, row_epoch); }
 void launch_erec_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* off, const uint32_t* deg,
-                      const uint32_t* adj, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anc, hipStream_t s)
+                      const uint32_t* adj, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anc, RecFmt rf,
+                      hipStream_t s)
 {
     if (!k) return;
     if (WHARF_ROW_CHUNKED && pre)
-        hipLaunchKernelGGL(k_erec_rows_c, chunk_grid(), 256, 0, s, runs, pre, k, off, deg, adj, vrec, erec, rs, keep_anc);
+        hipLaunchKernelGGL(k_erec_rows_c, chunk_grid(), 256, 0, s, runs, pre, k, off, deg, adj, vrec, erec, rs, keep_anc,
+                           rf);
     else
-        hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, off, deg, adj, vrec, erec, rs, keep_anc);
+        hipLaunchKernelGGL(k_erec_rows, (unsigned)k, 256, 0, s, runs, off, deg, adj, vrec, erec, rs, keep_anc, rf);
 }
 void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, const uint64_t* noff, const uint32_t* deg,
                         const uint32_t* adj, const uint64_t* need, const uint64_t* gofs, uint64_t base, uint64_t* fdir,
@@ -3542,11 +3550,11 @@ void launch_filter_rows(const RunInfo* runs, uint64_t k, const uint32_t* pre, co
     }
 }
 void launch_patch_in_edges(const uint32_t* adj, uint64_t slots, const uint32_t* bitmap, const uint32_t* bloom,
-                           const ERec* vrec, ERec* erec, uint32_t rs, hipStream_t s)
+                           const ERec* vrec, ERec* erec, uint32_t rs, RecFmt rf, hipStream_t s)
 {
     if (!slots) return;
     const unsigned grid = (unsigned)std::min<uint64_t>((slots / 4 + 1023) / 1024 + 1, (uint64_t)cu_count() * 2);
-    hipLaunchKernelGGL(k_patch_in_edges, grid, 1024, 0, s, adj, slots, bitmap, bloom + kBloomWords, vrec, erec, rs);
+    hipLaunchKernelGGL(k_patch_in_edges, grid, 1024, 0, s, adj, slots, bitmap, bloom + kBloomWords, vrec, erec, rs, rf);
 }
 void launch_transpose(const uint32_t* in, uint64_t W, uint32_t L, uint32_t* out, hipStream_t s)
 {

@@ -411,6 +411,43 @@ PATHS = {"sorted/slack": ("sorted", "0", "0", "on", "1", "0", "on", "0", "1"),
          "sorted/plain-rows": ("sorted", "0", "0", "on", "0", "0", "on", "1", "0")}
 
 
+@pytest.mark.parametrize("rows", ["slack", "repack", "compact"])
+@pytest.mark.parametrize("rec", ["wide", "compact", "compact-escape"])
+@pytest.mark.parametrize("mode", ["det", "deepwalk"])
+def test_edge_record_layouts(W, monkeypatch, rows, rec, mode):
+    """DeepWalk and deterministic handles keep 8-B edge records when the ids and slot offsets fit
+    (RecFmt: v | off << vb | deg << (vb + ob), a degree of 2^db - 1 or more read from deg[v]); the
+    16-B layout (WHARF_COMPACT_REC=0) and the compact one with a 4-bit degree field (every row of
+    degree >= 15 takes the escape) give the oracle's corpus, affected ids, counters and CSR through a
+    stream of RMAT batches, across pool repacks (records rebuilt for the new pool) and in-place
+    compactions; the records take 8 B per pool slot instead of 16."""
+    if rec == "wide":
+        monkeypatch.setenv("WHARF_COMPACT_REC", "0")
+    if rec == "compact-escape":
+        monkeypatch.setenv("WHARF_COMPACT_DEG_BITS", "4")
+    if rows == "repack":
+        monkeypatch.setenv("WHARF_POOL_NO_HEADROOM", "1")
+    if rows == "compact":
+        monkeypatch.setenv("WHARF_REPACK_MEM_CAP", "1")
+        monkeypatch.setenv("WHARF_NO_ROW_SLACK", "1")
+        monkeypatch.setenv("WHARF_POOL_HEADROOM", "30000")
+    n = 1 << 12
+    off, adj = O.csr_from_edges(n, O.generate_batch_of_edges(30000, 2 * n, 47, False, False))
+    kw = dict(deterministic=True) if mode == "det" else dict(deterministic=False, seed=13, model=0)
+    batches = []
+    for b in range(3):
+        e = O.generate_batch_of_edges(600, n, 50 + b, False, False)
+        batches += [(True, e, O.REMOVE_DUPS | O.APPLY_WALK_UPDATES), (False, e, O.REMOVE_DUPS | O.APPLY_WALK_UPDATES)]
+    batches.append((True, O.generate_batch_of_edges(900, n, 60, False, False), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES))
+    batches.append((True, O.generate_batch_of_edges(200, n, 61, False, True), O.REMOVE_DUPS | O.APPLY_WALK_UPDATES))
+    g = W.WharfMH.from_csr(off, adj, config=W.WharfConfig(walks_per_vertex=3, walk_length=24, **kw))
+    cap = g.stats()["pool_capacity"]
+    rec_bytes = g.memory_footprint(verbose=False)["records_bytes"] - 16 * n
+    assert rec_bytes == (16 if rec == "wide" else 8) * cap
+    g.destroy()
+    _compare_stream(W, off, adj, batches, wpv=3, L=24, **kw)
+
+
 @pytest.mark.parametrize("path", list(PATHS))
 @pytest.mark.parametrize("mode", ["det", "deepwalk", "node2vec"])
 def test_rewalk_and_update_paths(W, monkeypatch, path, mode):

@@ -33,6 +33,11 @@ for l in open(sys.argv[1]):
         rw = n2v.get('rewalk_latency_10k_batch') or {}
         print('headline', d.get('value'), 'mh_node2vec first/warm gen ms', n2v.get('first_generation_kernel_ms'),
               n2v.get('warm_generation_kernel_ms'), 'n2v rewalk median ms', rw.get('median_ms'))
+        c2, c2d = d.get('rewalk_latency_10k_batch') or {}, d.get('rewalk_latency_10k_batch_deterministic') or {}
+        probes = ((d.get('roofline') or {}).get('gather_ceiling') or {}).get('probes')
+        print('configs2 MH / det median ms', c2.get('median_ms'), c2d.get('median_ms'), 'rewalk kernel',
+              c2.get('median_rewalk_kernel_ms'), c2d.get('median_rewalk_kernel_ms'), 'gen same graph',
+              (c2.get('generation_same_graph') or {}).get('ms'), 'probes', probes)
 PYEOF
         [ $rc -eq 0 ] || exit $rc
     done
