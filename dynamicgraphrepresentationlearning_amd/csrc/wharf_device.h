@@ -171,7 +171,11 @@ __device__ __forceinline__ Row unpack_rec8(uint64_t q, RecFmt f, const uint32_t*
     r.v = (uint32_t)(q & ((1ull << f.vb) - 1));
     r.off = (q >> f.vb) & ((1ull << f.ob) - 1);
     const uint64_t d = q >> (f.vb + f.ob);
+#ifdef WHARF_PROBE_NO_ESCAPE   // timing probe only (hub degrees clipped: wrong walks)
+    r.deg = (uint32_t)d;
+#else
     r.deg = d == dmax ? deg[r.v] : (uint32_t)d;   // the escape: a hub's degree from its row
+#endif
     r.epoch = 0;
     return r;
 }

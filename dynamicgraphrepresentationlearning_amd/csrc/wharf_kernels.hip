@@ -410,13 +410,21 @@ struct Walker {
     uint64_t anc;    // node2vec MH: anchor entry of that slot
 };
 
-template <int MODEL, bool DET>
+// RL: the edge-record layout fixed at compile time -- 0 the 16-B records, 1 the compact 8-B ones
+// (a.rf) -- or -1, read from a.rf per load.  The hot kernels (k_walk, k_rewalk_sweep) are
+// instantiated per layout: a per-step branch on a.rf changed the lock-step sweep's code layout
+// and cost the 16-B path ~30 % (configs[3] re-walk 18 -> 24.5 ms, profiles/r06/compact_rec).
+template <int MODEL, bool DET, int RL = -1>
 __device__ __forceinline__ Row load_edge(const WalkArgs& a, uint64_t e, uint64_t& anc)
 {
     if constexpr (kRecStride<MODEL, DET> == 2) {
         const Row r = load_rec(a.erec, e * 2);
         anc = a.anchor[e * kAnchorStride];   // same 32-B record
         return r;
+    } else if constexpr (RL == 0) {
+        return load_rec(a.erec, e);
+    } else if constexpr (RL == 1) {
+        return unpack_rec8(reinterpret_cast<const uint64_t*>(a.erec)[e], a.rf, a.deg);
     } else {
         return load_erec(a.erec, e, 1, a.rf, a.deg);   // 16 B, or 8 B (compact)
     }
@@ -430,7 +438,7 @@ __device__ __forceinline__ Row load_edge(const WalkArgs& a, uint64_t e, uint64_t
 // not cached and is needed for the decision is not initialised here; the step
 // returns with `parked` set and the walker unchanged, and k_park_init computes
 // the anchor with full waves before the walker resumes.
-template <int MODEL, bool DET, bool PARK = false, bool RF = false>
+template <int MODEL, bool DET, bool PARK = false, bool RF = false, int RL = -1>
 __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, const uint64_t* __restrict__ rt,
                                               uint32_t pos, uint32_t wlo, uint32_t whi, uint32_t ep, uint32_t& accepts,
                                               uint32_t& inits, bool* parked = nullptr)
@@ -438,12 +446,13 @@ __device__ __forceinline__ uint32_t walk_step(const WalkArgs& a, Walker& w, cons
     Row nx;
     if constexpr (DET) {
         // rt = Random(wid / n) restarted at the walk's first re-walked position
-        nx = load_erec(a.erec, w.rc.off + umod64_32(rt[pos], w.rc.deg), 1, a.rf, a.deg);
+        uint64_t unused_anc;
+        nx = load_edge<MODEL, DET, RL>(a, w.rc.off + umod64_32(rt[pos], w.rc.deg), unused_anc);
     } else {
         const P4 q = philox4x32_10(wlo, whi, pos, ep | kStreamStep, a.key0, a.key1);
         const uint32_t ci = (uint32_t)pick32(q.x0, w.rc.deg);
         uint64_t canc = kAnchorNone64;
-        const Row cand = load_edge<MODEL, DET>(a, w.rc.off + ci, canc);
+        const Row cand = load_edge<MODEL, DET, RL>(a, w.rc.off + ci, canc);
         if constexpr (MODEL == kDeepWalk) {
             accepts++;   // weights are all 1: sample() always accepts
             nx = cand;
@@ -784,7 +793,7 @@ __device__ __forceinline__ uint32_t start_vertex(const WalkArgs& a, uint64_t j)
     return (uint32_t)(a.lo + j);
 }
 
-template <int MODEL, bool DET, bool BLK = false>
+template <int MODEL, bool DET, bool BLK = false, int RL = -1>
 __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
 {
     uint32_t steps = 0, accepts = 0, inits = 0;
@@ -803,7 +812,8 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
         uint32_t pos = 0;
         for (; pos + 1 < a.L; pos++) {
             if (w.rc.deg == 0) break;   // dead end: the walk stops (reference: lrand() % 0)
-            walks[(uint64_t)(pos + 1) * W + li] = walk_step<MODEL, DET>(a, w, rt, pos, wlo, whi, ep, accepts, inits);
+            walks[(uint64_t)(pos + 1) * W + li] =
+                walk_step<MODEL, DET, false, false, RL>(a, w, rt, pos, wlo, whi, ep, accepts, inits);
             steps++;
         }
         for (pos = pos + 1; pos < a.L; pos++) walks[(uint64_t)pos * W + li] = kSent;
@@ -845,7 +855,7 @@ __device__ __forceinline__ bool is_source(const WalkArgs& a, const uint32_t* s_b
     return (a.bitmap[x >> 5] >> (x & 31)) & 1u;
 }
 
-template <int MODEL, bool DET, bool BLK = false>
+template <int MODEL, bool DET, bool BLK = false, int RL = -1>
 __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
 {
     __shared__ uint32_t s_bloom[kBloomWords];
@@ -874,7 +884,8 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
             bool fresh = false;
             if (mode == kLaneWalk) {
                 if (w.rc.deg) {
-                    val = walk_step<MODEL, DET>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep, accepts, inits);
+                    val = walk_step<MODEL, DET, false, false, RL>(a, w, rt, DET ? pos - 1 - p : pos - 1, wlo, whi, ep,
+                                                                  accepts, inits);
                     steps++;
                 }
                 fresh = true;
@@ -2067,6 +2078,7 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
     const char* pk = getenv("WHARF_PLAN_KERNEL");
     const bool plan_lean = !(pk && std::string(pk) == "chunked") && a.W <= kLeanMaxW;
     const dim3 pgrid((unsigned)std::min<uint64_t>((a.W + 1023) / 1024, (uint64_t)cu_count() * 2));
+    const bool cr = a.rf.compact != 0;   // compact 8-B edge records (never with node2vec MH's anchors)
 #define WHARF_LAUNCH(M, D)                                                                   \
     do {                                                                                     \
         if (rewalk && M == kNode2Vec) {                                                      \
@@ -2085,11 +2097,15 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
                 else hipLaunchKernelGGL((k_rewalk_sorted<M, D>), lgrid, block, 0, s, a);     \
             }                                                                                \
         } else if (rewalk) {                                                                 \
-            if (a.sh_parts > 1) hipLaunchKernelGGL((k_rewalk_sweep<M, D, true>), grid, block, 0, s, a); \
-            else hipLaunchKernelGGL((k_rewalk_sweep<M, D>), grid, block, 0, s, a);           \
+            if (cr && a.sh_parts > 1) hipLaunchKernelGGL((k_rewalk_sweep<M, D, true, 1>), grid, block, 0, s, a); \
+            else if (cr) hipLaunchKernelGGL((k_rewalk_sweep<M, D, false, 1>), grid, block, 0, s, a); \
+            else if (a.sh_parts > 1) hipLaunchKernelGGL((k_rewalk_sweep<M, D, true, 0>), grid, block, 0, s, a); \
+            else hipLaunchKernelGGL((k_rewalk_sweep<M, D, false, 0>), grid, block, 0, s, a);     \
         } else {                                                                             \
-            if (a.sh_parts > 1) hipLaunchKernelGGL((k_walk<M, D, true>), grid, block, 0, s, a); \
-            else hipLaunchKernelGGL((k_walk<M, D>), grid, block, 0, s, a);                   \
+            if (cr && a.sh_parts > 1) hipLaunchKernelGGL((k_walk<M, D, true, 1>), grid, block, 0, s, a); \
+            else if (cr) hipLaunchKernelGGL((k_walk<M, D, false, 1>), grid, block, 0, s, a); \
+            else if (a.sh_parts > 1) hipLaunchKernelGGL((k_walk<M, D, true, 0>), grid, block, 0, s, a); \
+            else hipLaunchKernelGGL((k_walk<M, D, false, 0>), grid, block, 0, s, a);         \
         }                                                                                    \
     } while (0)
     // a multiple of 8 workgroups: every XCD gets the same number
