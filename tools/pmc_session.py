@@ -80,14 +80,14 @@ def main():
     line = bench_line(os.path.join(sess, "prof_bench.log"))
     shutil.copy(os.path.join(sess, "prof_bench.log"), os.path.join(out_dir, "prof_bench.log"))
     steps = line["config"]["transitions_per_step"]
-    gen = summary("k_walk<0, false, false>", pmc["pmc_gen_fetch"], pmc["pmc_gen_write"], tr, dur_slice=slice(2, 7),
+    gen = summary("k_walk<0, false, false", pmc["pmc_gen_fetch"], pmc["pmc_gen_write"], tr, dur_slice=slice(2, 7),
                   algorithmic=steps * 24)
     gen["bench_line_avg_kernel_ms_same_run"] = line["roofline"]["avg_kernel_ms"]
     gen["bench_line_value_same_run"] = line["value"]
     out = {
         f"{rnd}_gen_deepwalk_mh_s22": gen,
         # node2vec: the first launch also fills the anchor cache; warm launches only
-        f"{rnd}_gen_node2vec_mh_s22": summary("k_walk<1, false, false>", pmc["pmc_gen_fetch"], pmc["pmc_gen_write"], tr,
+        f"{rnd}_gen_node2vec_mh_s22": summary("k_walk<1, false, false", pmc["pmc_gen_fetch"], pmc["pmc_gen_write"], tr,
                                               skip=1, dur_slice=slice(1, 4)),
     }
     str_trace = os.path.join(sess, "prof_str", "run_kernel_trace.csv")
