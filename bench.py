@@ -116,7 +116,7 @@ def balanced_shards(deg: np.ndarray, parts: int):
     return bs(deg, parts)
 
 
-def measure_gather_ceiling(runs: int = 3):
+def measure_gather_ceiling(runs: int = 3, gib: float = 3.48):
     """The chip's dependent random 16-B gather rate with the walk kernel's shape
     (41.9 M lanes x 79 dependent gathers from a 3.5 GiB table), measured on this
     box by tools/gather_roof `runs` times BEFORE the timed region, on an idle
@@ -128,7 +128,7 @@ def measure_gather_ceiling(runs: int = 3):
     rates = []
     for _ in range(runs):
         try:
-            r = subprocess.run([exe, "3.48", "coarse", "dep"], capture_output=True, text=True, timeout=180)
+            r = subprocess.run([exe, f"{gib:.2f}", "coarse", "dep"], capture_output=True, text=True, timeout=180)
             for line in r.stdout.splitlines():
                 if line.startswith("{"):
                     rates.append(float(json.loads(line)["Ggathers_per_s"]))
@@ -137,7 +137,7 @@ def measure_gather_ceiling(runs: int = 3):
     return rates or None
 
 
-def gather_ceiling(steps_per_s: float, live):
+def gather_ceiling(steps_per_s: float, live, matched=None):
     """The generation kernel against the box's random-gather rate (one dependent
     16-B gather per step), probed before the timed region: min / max of the
     probes and the kernel's rate as a fraction of each.  A fraction above 1 is
@@ -146,9 +146,18 @@ def gather_ceiling(steps_per_s: float, live):
     if not live:
         return None
     lo, hi = min(live), max(live)
-    return {"Ggathers_per_s_min": round(lo, 2), "Ggathers_per_s_max": round(hi, 2), "probes": [round(x, 2) for x in live],
-            "frac_of_min": round(steps_per_s / (lo * 1e9), 4), "frac_of_max": round(steps_per_s / (hi * 1e9), 4),
-            "source": "tools/gather_roof 3.48 coarse dep, this box, before the timed region"}
+    rec = {"Ggathers_per_s_min": round(lo, 2), "Ggathers_per_s_max": round(hi, 2), "probes": [round(x, 2) for x in live],
+           "frac_of_min": round(steps_per_s / (lo * 1e9), 4), "frac_of_max": round(steps_per_s / (hi * 1e9), 4),
+           "source": "tools/gather_roof 3.48 coarse dep (16-B records, the box's yardstick), this box, before the "
+                     "timed region"}
+    if matched and matched.get("probes"):
+        mp = matched["probes"]
+        rec["table_matched"] = {"table_GiB": matched["table_GiB"], "probes": [round(x, 2) for x in mp],
+                                "frac_of_min": round(steps_per_s / (min(mp) * 1e9), 4),
+                                "frac_of_max": round(steps_per_s / (max(mp) * 1e9), 4),
+                                "source": "tools/gather_roof <the graph's edge-record table size> coarse dep, after "
+                                          "the graph is built, before the timed region"}
+    return rec
 
 
 PMC_ROUNDS = ("r06_", "r05_", "r04_", "r03_", "r02_", "")   # newest round's rocprofv3 summary first
@@ -1139,6 +1148,14 @@ def main():
     g.set_shard(lo, hi)
     m = g.number_of_edges()
     log(f"[rank {rank}] graph n={n} m={m} built in {time.time() - t0:.1f}s; shard [{lo},{hi}), wpv={wpv}")
+    # the same probe over a table the size of this graph's edge records (8 B per slot when compact, 16 B
+    # otherwise): the 3.48-GiB probe above is the box's yardstick, this one the kernel's own table size
+    matched = None
+    if live_ceiling:
+        table_gib = (g.memory_footprint(verbose=False)["records_bytes"] - 16 * n) / 2 ** 30
+        matched = {"table_GiB": round(table_gib, 3),
+                   "probes": measure_gather_ceiling(args.gather_probes, table_gib)}
+        log(f"gather_roof probes at the record table's size ({table_gib:.2f} GiB): {matched['probes']}")
 
     def barrier():
         if dist:
@@ -1255,7 +1272,7 @@ def main():
                          "avg_kernel_ms": round(avg_kernel_ms, 3),
                          # the first generation of a fresh handle (node2vec: every anchor initialised)
                          "first_generation_kernel_ms": round(warm_ms[0], 3) if warm_ms else None,
-                         "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3), live_ceiling)
+                         "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3), live_ceiling, matched)
                          if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None},
             "per_gpu_of_8": per8,
             "jobs_8gpu": jobs,
