@@ -793,6 +793,27 @@ __device__ __forceinline__ uint32_t start_vertex(const WalkArgs& a, uint64_t j)
     return (uint32_t)(a.lo + j);
 }
 
+// The walk matrix written (k_walk, k_rewalk_sweep) and scanned (k_rewalk_sweep) with non-temporal
+// stores and loads (round 6), so the streamed matrix displaces fewer of the edge-record lines the
+// gathers hit in the Infinity Cache: same-box A/B, 3 reps, headline +0.4 %, configs[2] DeepWalk MH
+// re-walk -3 % (profiles/r06/nt_walks/).  0 / 0 restores plain accesses (A/B).
+#ifndef WHARF_NT_WALK_STORES
+#define WHARF_NT_WALK_STORES 1
+#endif
+#ifndef WHARF_NT_SWEEP_LOADS
+#define WHARF_NT_SWEEP_LOADS 1
+#endif
+__device__ __forceinline__ void put_walk(uint32_t* p, uint32_t v)
+{
+    if (WHARF_NT_WALK_STORES) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ uint32_t get_walk(const uint32_t* p)
+{
+    if (WHARF_NT_SWEEP_LOADS) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
 template <int MODEL, bool DET, bool BLK = false, int RL = -1>
 __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
 {
@@ -812,8 +833,8 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a)
         uint32_t pos = 0;
         for (; pos + 1 < a.L; pos++) {
             if (w.rc.deg == 0) break;   // dead end: the walk stops (reference: lrand() % 0)
-            walks[(uint64_t)(pos + 1) * W + li] =
-                walk_step<MODEL, DET, false, false, RL>(a, w, rt, pos, wlo, whi, ep, accepts, inits);
+            put_walk(walks + (uint64_t)(pos + 1) * W + li,
+                     walk_step<MODEL, DET, false, false, RL>(a, w, rt, pos, wlo, whi, ep, accepts, inits));
             steps++;
         }
         for (pos = pos + 1; pos < a.L; pos++) walks[(uint64_t)pos * W + li] = kSent;
@@ -893,7 +914,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
                 if (pos > 0) {
                     xprev = x;
                     x = xn;
-                    if (pos + 1 < L && x != kSent) xn = walks[(uint64_t)(pos + 1) * W + li];
+                    if (pos + 1 < L && x != kSent) xn = get_walk(walks + (uint64_t)(pos + 1) * W + li);
                 }
                 val = x;
                 if (x == kSent) {
@@ -907,7 +928,7 @@ __global__ __launch_bounds__(256) void k_rewalk_sweep(WalkArgs a)
             if (!a.scan_only && __any(fresh)) {
                 // kLaneDone lanes: unaffected (their old walk is kSent from
                 // here on) — the same value is rewritten
-                walks[(uint64_t)pos * W + li] = val;
+                put_walk(walks + (uint64_t)pos * W + li, val);
             }
             if (!__any(mode != kLaneDone)) break;
         }
