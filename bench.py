@@ -90,6 +90,7 @@ def parse():
     p.add_argument("--per-gpu-of-8", type=int, default=1,
                    help="configs[3] / configs[4]: the per-GPU work of their 8-GPU runs on this GPU (0 = off)")
     p.add_argument("--per8-batches", type=int, default=5, help="update batches per per_gpu_of_8 case")
+    p.add_argument("--per8-cases", default="", help="comma list of per_gpu_of_8 case names to run ('' = all; A/B runs)")
     p.add_argument("--jobs", default="configs3,configs4",
                    help="at N > 1: BASELINE's 8-GPU jobs run on the ranks of this run (comma list; '' = none)")
     p.add_argument("--job-batches", type=int, default=5, help="update batches per job (configs[4]: insert+delete pairs)")
@@ -711,6 +712,9 @@ def per_gpu_of_8(args, W, torch, dev, barrier):
              ("configs3_deepwalk_det_shard0of8", 25, 1_200_000_000, W.DEEPWALK, True, 8, False),
              ("configs3_deepwalk_mh_all_walks_1gpu", 25, 1_200_000_000, W.DEEPWALK, False, 1, False),
              ("configs4_node2vec_mh_shard0of8", 26, 1_800_000_000, W.NODE2VEC, False, 8, True)]
+    if args.per8_cases:
+        keep = set(args.per8_cases.split(","))
+        cases = [c for c in cases if c[0] in keep]
     for name, scale, samples, model, det, parts, mixed in cases:
         n = 1 << scale
         g = None
