@@ -645,7 +645,9 @@ struct wharf_handle {
         if (anchors || (e && *e && atoi(e) == 0)) return RecFmt{0u, 0u, 0u};
         const uint32_t vb = std::max<uint32_t>(bits_for(std::max<uint64_t>(n, 2)), 1);
         uint32_t ob = std::max<uint32_t>(bits_for(std::max<uint64_t>(pc, 2)), 1);
-        if (vb + ob + kMinCompactDegBits > 64) return RecFmt{0u, 0u, 0u};
+        const char* mdb = getenv("WHARF_COMPACT_MIN_DEG_BITS");   // A/B: allow a narrower degree field
+        const uint32_t min_db = mdb && *mdb ? (uint32_t)std::max(atoi(mdb), 1) : kMinCompactDegBits;
+        if (vb + ob + min_db > 64) return RecFmt{0u, 0u, 0u};
         const char* db = getenv("WHARF_COMPACT_DEG_BITS");   // tests: a narrow degree field, so rows of
         if (db && *db) {                                     // degree >= 2^db - 1 take the escape
             const uint32_t d = std::min<uint32_t>(std::max<int>(atoi(db), 1), 32);
