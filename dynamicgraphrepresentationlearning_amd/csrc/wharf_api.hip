@@ -2,6 +2,7 @@
 // the graph / batch pipelines (rocPRIM sorts, selects and scans on the
 // handle's stream) and the host side of every entry point.
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -1537,6 +1538,37 @@ int wharf_release_caches(wharf_handle* h, uint64_t* freed_bytes)
     });
 }
 
+// The line-count model behind the up-front init order (k_anchor_init_all / k_anchor_init_cur): 21
+// uniform proposals over L 128-B lines touch L (1 - (1 - 1/L)^21) distinct lines.  Prev order pays
+// that over cur's row (4 B per slot: 32 slots per line); cur order pays it over prev's neighbour
+// filter (2^lg 32-bit words: 32 per line), plus prev's filter descriptor and the entry written at
+// the reverse slot.  t[lg] = the fewest lines of cur's row at which cur order is cheaper.
+// WHARF_INIT_CUR_BIAS (lines, A/B and tests) is added to the cur-order side.
+static InitOrder init_order_table(const WalkArgs& a)
+{
+    auto distinct = [](double L) { return L <= 1.0 ? 1.0 : L * (1.0 - std::pow(1.0 - 1.0 / L, (double)kWeightProposals)); };
+    const char* b = getenv("WHARF_INIT_CUR_BIAS");
+    const double bias = b && *b ? atof(b) : 0.0;
+    const bool use_f = a.fpool && a.inv_q != 1.0f;
+    InitOrder ord;
+    for (uint32_t lg = 0; lg < kInitOrderLg; lg++) {
+        const double filt_lines = std::max(1.0, std::ldexp(1.0, (int)lg) / 32.0);
+        const double cur_cost = 1.0 + (use_f ? 1.0 + distinct(filt_lines) : 0.0) + bias;
+        uint64_t lo = 1, hi = 1;
+        while (hi < (1ull << 32) && distinct((double)hi) <= cur_cost) hi <<= 1;
+        if (distinct((double)hi) <= cur_cost) {
+            ord.t[lg] = 0xFFFFFFFFu;   // never cheaper (D < 21 for every row)
+            continue;
+        }
+        while (lo < hi) {   // the least L with distinct(L) > cur_cost
+            const uint64_t mid = (lo + hi) / 2;
+            if (distinct((double)mid) > cur_cost) hi = mid; else lo = mid + 1;
+        }
+        ord.t[lg] = (uint32_t)lo;
+    }
+    return ord;
+}
+
 int wharf_generate(wharf_handle* h)
 {
     return guarded(h, [&] {
@@ -1588,7 +1620,13 @@ int wharf_generate(wharf_handle* h)
                 const bool by_cur = h->symmetric && bc && *bc && atoi(bc) != 0;
                 const uint32_t ty = by_cur ? (bcy && *bcy ? (uint32_t)atoi(bcy) : 256u) : 0u;
                 const uint32_t tx = bcx && *bcx ? (uint32_t)atoi(bcx) : 256u;
-                launch_anchor_init_all(a, ow, h->pool_used, ty, tx, h->s);
+                // round 6: with the reverse-slot index every state goes to the cheaper order
+                // (init_order_table; WHARF_INIT_ORDER=0: all in prev order, or the round-5 rule above)
+                const char* io = getenv("WHARF_INIT_ORDER");
+                const bool hybrid = h->symmetric && h->rev_on && h->rev.p && !(io && *io && atoi(io) == 0);
+                const char* rvf = getenv("WHARF_REV_VERIFY");
+                launch_anchor_init_all(a, ow, h->pool_used, ty, tx, hybrid ? h->rev.as<uint32_t>() : nullptr,
+                                       init_order_table(a), rvf && *rvf && atoi(rvf) != 0, h->s);
                 HIPCHK(hipStreamSynchronize(h->s));   // before the owner buffer is released
                 owner.release();
             }

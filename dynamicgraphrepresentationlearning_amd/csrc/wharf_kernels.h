@@ -98,10 +98,22 @@ void launch_src_index(const RunInfo* runs, uint64_t k, uint32_t* src_idx, hipStr
 void launch_source_degrees(const RunInfo* runs, uint64_t k, const ERec* vrec, uint64_t* out, hipStream_t s);
 void launch_anchor_preinit(const WalkArgs& a, const uint64_t* preoff, uint64_t k, hipStream_t s);
 void launch_slot_owner_fill(const uint64_t* off, const uint32_t* deg, uint64_t n, uint32_t* owner, hipStream_t s);
+// Which order computes a state's anchor up front (round 6, undirected graphs with the reverse-slot
+// index): state (cur y, prev x) goes in cur order iff cur's row spans at least t[lg(x)] 128-B lines,
+// lg(x) = filt_log2_words(deg x) (the size of prev's neighbour filter).  The host fills t from a
+// line-count model (wharf_api.hip, init_order_table); integers, so both kernels decide alike.
+constexpr uint32_t kWeightProposals = 21;   // WEIGHT inits: the best of 21 proposals (metropolis_hastings_sampler.h:87-107)
+constexpr uint32_t kInitOrderLg = 40;
+struct InitOrder {
+    uint32_t t[kInitOrderLg];
+};
 // by_cur_y != 0 (undirected graphs): the states of hub curs (deg > by_cur_y) with small prevs
-// (deg <= by_cur_x) computed in cur order by a second kernel (k_anchor_init_by_cur)
+// (deg <= by_cur_x) computed in cur order by a second kernel (k_anchor_init_by_cur, round 5).
+// ridx != null (undirected, reverse-slot index): every state in the cheaper of the two orders by
+// `ord` (k_anchor_init_all + k_anchor_init_cur); verify: check each reverse slot before writing.
 void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t slots, uint32_t by_cur_y,
-                            uint32_t by_cur_x, hipStream_t s);
+                            uint32_t by_cur_x, const uint32_t* ridx, const InitOrder& ord, bool verify,
+                            hipStream_t s);
 void launch_vrec(const uint64_t* off, const uint32_t* deg, uint64_t n, const uint32_t* row_epoch, ERec* vrec,
                  hipStream_t s);
 void launch_erec(const uint32_t* adj, uint64_t slots, const ERec* vrec, ERec* erec, uint32_t rs, int keep_anchors,

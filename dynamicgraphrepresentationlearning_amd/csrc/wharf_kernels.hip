@@ -129,7 +129,6 @@ __device__ __forceinline__ float weight(const WalkArgs& a, const Row& rprev, uin
 // and BURNIN, one lane at a time.  Returns the anchor as a slot of cur's row,
 // and its weight class.  WEIGHT (best of 1 + 20 proposals) is evaluated by
 // the whole wave: anchor_init_wave below.
-constexpr uint32_t kWeightProposals = 21;
 
 __device__ uint32_t anchor_init(const WalkArgs& a, const Row& rc, const Row& rp, uint32_t& cls)
 {
@@ -691,26 +690,86 @@ __global__ __launch_bounds__(256) void k_slot_owner_fill(const uint64_t* __restr
     }
 }
 
+// The up-front inits in two orders (round 6, undirected graphs with the reverse-slot index).  A
+// state (y, x) -- cur y, prev x, its entry on slot x -> y -- costs random 128-B lines on one side:
+// in prev order (lanes over x's row, x's filter words and row record shared by the wave) the 21
+// proposals' targets land in y's row, ~min(21, lines of y's row) distinct lines; in cur order
+// (lanes over y's row, y's row shared) they are x's filter words, ~min(21, lines of x's filter),
+// plus x's filter descriptor and the entry written at the reverse slot.  Each state goes to the
+// cheaper side by InitOrder (a table the host fills from that model): cur order iff y's row spans
+// at least t[filt_log2_words(deg x)] lines.  Prev-order lanes read y's row record from the slot's
+// own edge record (coalesced, 32-B node2vec records) instead of vrec[y] (one random line each);
+// cur-order lanes read x's record from the slot y -> x likewise.  XCD-aware: a window of the
+// grid-stride loop is dealt to the 8 XCDs in contiguous eighths, so each row's lines are fetched
+// into one XCD's L2.  Same anchors, one init per state.
+__device__ __forceinline__ uint64_t init_block_index()
+{
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    return nb % 8 == 0 ? (uint64_t)(b % 8) * (nb / 8) + b / 8 : b;   // dispatch deals blocks to XCDs round-robin
+}
+__device__ __forceinline__ bool init_in_cur_order(const InitOrder& ord, uint32_t dcur, uint32_t dprev)
+{
+    const uint32_t lg = min(filt_log2_words(dprev), kInitOrderLg - 1);
+    return ((uint64_t)dcur + 31) / 32 >= ord.t[lg];
+}
+
 // by_cur_y / by_cur_x (round 5, undirected graphs): the states (y, x) with deg(y) > by_cur_y and
-// deg(x) <= by_cur_x are left to k_anchor_init_by_cur (0: none are)
+// deg(x) <= by_cur_x are left to k_anchor_init_by_cur (0: none are).  hybrid: the states
+// init_in_cur_order selects are left to k_anchor_init_cur.
 __global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint32_t* __restrict__ owner, uint64_t slots,
-                                                         uint32_t by_cur_y, uint32_t by_cur_x)
+                                                         uint32_t by_cur_y, uint32_t by_cur_x, bool hybrid,
+                                                         InitOrder ord)
 {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t inits = 0;
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < slots; e += stride) {
+    for (uint64_t e = init_block_index() * blockDim.x + threadIdx.x; e < slots; e += stride) {
         const uint32_t y = a.adj[e], o = owner[e];
         bool need = y != kGap && o != 0;
         Row rx{}, ry{};
         if (need) {
             rx = load_rec(a.vrec, o - 1);
-            ry = load_rec(a.vrec, y);
+            ry = load_rec(a.erec, e * 2);   // y's row: slot e's own (32-B) record
             need = e < rx.off + rx.deg && ry.deg != 0;   // (slots past a row's end are kGap; the test is cheap)
             if (by_cur_y && ry.deg > by_cur_y && rx.deg <= by_cur_x) need = false;
+            if (hybrid && init_in_cur_order(ord, ry.deg, rx.deg)) need = false;
         }
         uint32_t an = 0, cls = 0;
         anchor_compute(a, need, ry, rx, an, cls, inits);
         if (need) a.anchor[e * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
+    }
+    wave_add(a.counters + 7, inits);
+}
+
+// The states init_in_cur_order selects, in cur order: one lane per slot f = y -> x of y's row (the
+// state (y, x)); x's row from f's own record; the entry written at slot x -> y = off(x) + ridx[f].
+// VERIFY (tests, WHARF_REV_VERIFY): the reverse slot is checked first, and a stale one is found by
+// a search instead.
+template <bool VERIFY>
+__global__ __launch_bounds__(256) void k_anchor_init_cur(WalkArgs a, const uint32_t* __restrict__ owner, uint64_t slots,
+                                                         const uint32_t* __restrict__ ridx, InitOrder ord)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t inits = 0;
+    for (uint64_t f = init_block_index() * blockDim.x + threadIdx.x; f < slots; f += stride) {
+        const uint32_t x = a.adj[f], o = owner[f];
+        bool need = x != kGap && o != 0;
+        Row ry{}, rx{};
+        int64_t ein = -1;
+        if (need) {
+            ry = load_rec(a.vrec, o - 1);   // cur: the row this slot belongs to (shared by the wave)
+            rx = load_rec(a.erec, f * 2);   // prev: slot f's own record
+            need = f < ry.off + ry.deg && rx.deg != 0 && init_in_cur_order(ord, ry.deg, rx.deg);
+            if (need) {
+                const uint32_t r = ridx[f];
+                ein = r == kNoRidx ? -1 : (int64_t)(rx.off + r);
+                if (VERIFY && ein >= 0 && (r >= rx.deg || a.adj[ein] != ry.v)) ein = -1;
+                if (ein < 0) ein = row_find(a.adj, rx, ry.v);
+                need = ein >= 0;   // (an undirected graph always has the slot x -> y)
+            }
+        }
+        uint32_t an = 0, cls = 0;
+        anchor_compute(a, need, ry, rx, an, cls, inits);
+        if (need) a.anchor[(uint64_t)ein * kAnchorStride] = ((uint64_t)cls << 62) | ((uint64_t)a.epoch << 32) | an;
     }
     wave_add(a.counters + 7, inits);
 }
@@ -724,7 +783,8 @@ __global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint3
 // hub cur's proposals are ~21 random lines per state.  Line model on RMAT at
 // configs[4]'s density (scale 20): 8.46 lines per state in prev order,
 // 6.66 with the states of hub y >= 256 and x <= 256 taken here.  Undirected graphs
-// only: the state (y, x) of slot x -> y is reached through slot y -> x.
+// only: the state (y, x) of slot x -> y is reached through slot y -> x.  (Round 5; without
+// the reverse-slot index only.)
 __global__ __launch_bounds__(256) void k_anchor_init_by_cur(WalkArgs a, const uint32_t* __restrict__ owner,
                                                             uint64_t slots, uint32_t by_cur_y, uint32_t by_cur_x)
 {
@@ -755,12 +815,18 @@ void launch_slot_owner_fill(const uint64_t* off, const uint32_t* deg, uint64_t n
 }
 
 void launch_anchor_init_all(const WalkArgs& a, const uint32_t* owner, uint64_t slots, uint32_t by_cur_y,
-                            uint32_t by_cur_x, hipStream_t s)
+                            uint32_t by_cur_x, const uint32_t* ridx, const InitOrder& ord, bool verify, hipStream_t s)
 {
     if (!slots) return;
-    hipLaunchKernelGGL(k_anchor_init_all, cu_count() * 8, 256, 0, s, a, owner, slots, by_cur_y, by_cur_x);
-    if (by_cur_y)
+    const bool hybrid = ridx != nullptr;
+    if (hybrid) by_cur_y = 0;
+    hipLaunchKernelGGL(k_anchor_init_all, cu_count() * 8, 256, 0, s, a, owner, slots, by_cur_y, by_cur_x, hybrid, ord);
+    if (hybrid) {
+        if (verify) hipLaunchKernelGGL(k_anchor_init_cur<true>, cu_count() * 8, 256, 0, s, a, owner, slots, ridx, ord);
+        else hipLaunchKernelGGL(k_anchor_init_cur<false>, cu_count() * 8, 256, 0, s, a, owner, slots, ridx, ord);
+    } else if (by_cur_y) {
         hipLaunchKernelGGL(k_anchor_init_by_cur, cu_count() * 8, 256, 0, s, a, owner, slots, by_cur_y, by_cur_x);
+    }
 }
 
 __global__ void k_source_degrees(const RunInfo* __restrict__ runs, uint64_t k, const ERec* __restrict__ vrec,

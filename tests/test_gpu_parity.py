@@ -203,7 +203,7 @@ def _compare_stream(W, off, adj, batches, wpv=3, L=12, **kw):
     g.destroy()
 
 
-@pytest.mark.parametrize("preinit_all", ["0", "1", "1-by-cur", "1-by-prev"])
+@pytest.mark.parametrize("preinit_all", ["0", "1", "1-by-cur", "1-by-prev", "1-hybrid", "1-hybrid-all"])
 @pytest.mark.parametrize("init", [1, 2])   # BURNIN, WEIGHT
 def test_node2vec_anchors_up_front_or_lazily(W, monkeypatch, preinit_all, init):
     """Every anchor computed at the first generation (round 4's rule: >= 1 walk step
@@ -213,8 +213,19 @@ def test_node2vec_anchors_up_front_or_lazily(W, monkeypatch, preinit_all, init):
     and deletes, so the re-walks run into states no walker had entered.  Up
     front, the states of hub curs with small prevs are computed in cur order
     (k_anchor_init_by_cur; 1-by-cur: thresholds lowered so that most states go
-    that way) or all in prev order (1-by-prev: WHARF_INIT_BY_CUR=0)."""
+    that way) or all in prev order (1-by-prev: WHARF_INIT_BY_CUR=0).  With the reverse-slot
+    index (1-hybrid*, WHARF_REV=1) each state goes to the cheaper order by the line model
+    (k_anchor_init_all + k_anchor_init_cur); the bias moves the small test graph's states to
+    cur order when their cur's row spans 2+ lines (1-hybrid) or all of them (1-hybrid-all), and
+    the reverse slots are verified (conftest: WHARF_REV_VERIFY=1)."""
     monkeypatch.setenv("WHARF_PREINIT_ALL", preinit_all[0])
+    hybrid = preinit_all.startswith("1-hybrid")
+    if hybrid:
+        monkeypatch.setenv("WHARF_REV", "1")
+        monkeypatch.setenv("WHARF_INIT_CUR_BIAS", "-100" if preinit_all == "1-hybrid-all" else "-1.5")
+    else:
+        monkeypatch.delenv("WHARF_REV", raising=False)
+        monkeypatch.delenv("WHARF_INIT_CUR_BIAS", raising=False)
     monkeypatch.setenv("WHARF_NO_PREINIT", "")
     monkeypatch.setenv("WHARF_INIT_BY_CUR", "0" if preinit_all == "1-by-prev" else "1")
     monkeypatch.setenv("WHARF_INIT_BY_CUR_Y", "4" if preinit_all == "1-by-cur" else "")
@@ -234,8 +245,16 @@ def test_node2vec_anchors_up_front_or_lazily(W, monkeypatch, preinit_all, init):
                                                           sampler_init=init))
     g.generate_initial_random_walks()
     inits = g.stats()["last_anchor_inits"]
+    csr_bytes = g.memory_footprint(verbose=False)["csr_bytes"]
     g.destroy()
     assert (inits == len(adj)) if preinit_all != "0" else (0 < inits != len(adj)), (inits, len(adj))
+    if hybrid:   # the two-order path needs the reverse-slot index: it was there (4 B per slot)
+        monkeypatch.setenv("WHARF_REV", "0")
+        g0 = W.WharfMH.from_csr(off, adj, config=W.WharfConfig(walks_per_vertex=1, walk_length=20, deterministic=False,
+                                                               seed=17, model=1, paramP=0.5, paramQ=2.0,
+                                                               sampler_init=init))
+        assert csr_bytes >= g0.memory_footprint(verbose=False)["csr_bytes"] + 4 * len(adj)
+        g0.destroy()
 
 
 def test_edge_cases_isolated_dead_ends_and_flags(W):
