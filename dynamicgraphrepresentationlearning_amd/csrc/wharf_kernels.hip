@@ -702,10 +702,23 @@ __global__ __launch_bounds__(256) void k_slot_owner_fill(const uint64_t* __restr
 // cur-order lanes read x's record from the slot y -> x likewise.  XCD-aware: a window of the
 // grid-stride loop is dealt to the 8 XCDs in contiguous eighths, so each row's lines are fetched
 // into one XCD's L2.  Same anchors, one init per state.
-__device__ __forceinline__ uint64_t init_block_index()
+#ifndef WHARF_INIT_XCD_SPAN
+#define WHARF_INIT_XCD_SPAN 0   // A/B: 1 = each XCD takes one contiguous eighth of all slots, 2 = plain order
+#endif
+struct SlotLoop {
+    uint64_t i, end, step;
+};
+__device__ __forceinline__ SlotLoop init_slot_loop(uint64_t slots)
 {
-    const uint32_t nb = gridDim.x, b = blockIdx.x;
-    return nb % 8 == 0 ? (uint64_t)(b % 8) * (nb / 8) + b / 8 : b;   // dispatch deals blocks to XCDs round-robin
+    const uint32_t nb = gridDim.x, b = blockIdx.x;   // dispatch deals blocks to XCDs round-robin
+    if (nb % 8 || WHARF_INIT_XCD_SPAN == 2) return SlotLoop{(uint64_t)b * blockDim.x + threadIdx.x, slots, (uint64_t)nb * blockDim.x};
+    if (WHARF_INIT_XCD_SPAN == 1) {
+        const uint64_t part = (slots + 7) / 8, lo = min(slots, (uint64_t)(b % 8) * part);
+        return SlotLoop{lo + (uint64_t)(b / 8) * blockDim.x + threadIdx.x, min(slots, lo + part),
+                        (uint64_t)(nb / 8) * blockDim.x};
+    }
+    return SlotLoop{((uint64_t)(b % 8) * (nb / 8) + b / 8) * blockDim.x + threadIdx.x, slots,
+                    (uint64_t)nb * blockDim.x};
 }
 __device__ __forceinline__ bool init_in_cur_order(const InitOrder& ord, uint32_t dcur, uint32_t dprev)
 {
@@ -720,9 +733,9 @@ __global__ __launch_bounds__(256) void k_anchor_init_all(WalkArgs a, const uint3
                                                          uint32_t by_cur_y, uint32_t by_cur_x, bool hybrid,
                                                          InitOrder ord)
 {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t inits = 0;
-    for (uint64_t e = init_block_index() * blockDim.x + threadIdx.x; e < slots; e += stride) {
+    for (SlotLoop l = init_slot_loop(slots); l.i < l.end; l.i += l.step) {
+        const uint64_t e = l.i;
         const uint32_t y = a.adj[e], o = owner[e];
         bool need = y != kGap && o != 0;
         Row rx{}, ry{};
@@ -748,9 +761,9 @@ template <bool VERIFY>
 __global__ __launch_bounds__(256) void k_anchor_init_cur(WalkArgs a, const uint32_t* __restrict__ owner, uint64_t slots,
                                                          const uint32_t* __restrict__ ridx, InitOrder ord)
 {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t inits = 0;
-    for (uint64_t f = init_block_index() * blockDim.x + threadIdx.x; f < slots; f += stride) {
+    for (SlotLoop l = init_slot_loop(slots); l.i < l.end; l.i += l.step) {
+        const uint64_t f = l.i;
         const uint32_t x = a.adj[f], o = owner[f];
         bool need = x != kGap && o != 0;
         Row ry{}, rx{};
