@@ -216,13 +216,15 @@ def test_node2vec_anchors_up_front_or_lazily(W, monkeypatch, preinit_all, init):
     that way) or all in prev order (1-by-prev: WHARF_INIT_BY_CUR=0).  With the reverse-slot
     index (1-hybrid*, WHARF_REV=1) each state goes to the cheaper order by the line model
     (k_anchor_init_all + k_anchor_init_cur); the bias moves the small test graph's states to
-    cur order when their cur's row spans 2+ lines (1-hybrid) or all of them (1-hybrid-all), and
-    the reverse slots are verified (conftest: WHARF_REV_VERIFY=1)."""
+    cur order when their cur's row spans 2+ lines (1-hybrid, reverse slots verified) or all of
+    them (1-hybrid-all, the production instantiation without the check)."""
     monkeypatch.setenv("WHARF_PREINIT_ALL", preinit_all[0])
     hybrid = preinit_all.startswith("1-hybrid")
     if hybrid:
         monkeypatch.setenv("WHARF_REV", "1")
         monkeypatch.setenv("WHARF_INIT_CUR_BIAS", "-100" if preinit_all == "1-hybrid-all" else "-1.5")
+        # the default (unverified) instantiation of k_anchor_init_cur too: the index is exact here
+        monkeypatch.setenv("WHARF_REV_VERIFY", "0" if preinit_all == "1-hybrid-all" else "1")
     else:
         monkeypatch.delenv("WHARF_REV", raising=False)
         monkeypatch.delenv("WHARF_INIT_CUR_BIAS", raising=False)
