@@ -458,6 +458,13 @@ def cpu_baseline_deterministic(args, batches=3):
                                                               * (args.length - 1) / (args.cpu_length - 1), 1)}
 
 
+def record_bytes_per_slot(g, n, anchors):
+    """Edge-record bytes per pool slot from the handle's footprint (vrec: 16 B per vertex)."""
+    per = (g.memory_footprint(verbose=False)["records_bytes"] - 16 * n) / max(g.stats()["pool_capacity"], 1)
+    per *= 2 if anchors else 1
+    return min((8, 16, 32), key=lambda b: abs(b - per))
+
+
 def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrier, batches, scan_batches=0):
     """configs[2]: per-batch latency of 10k-edge insert batches with the re-walk applied
     (memory-throughput-latency.cpp:126-134: generate_batch_of_edges(5000, n, seed=b, false, undirected))."""
@@ -529,7 +536,9 @@ def stream_latency(args, W, torch, cfg, dev, world, rank, dist, comm_dev, barrie
            # index (pool_slots = the sources' new row slots, at most)
            "in_edge_mode": "reverse_index" if np.median(imode) >= 1 else "scan",
            "stored_positions_rank0": int(gs.number_of_walks) * args.length,
-           "record_bytes": 32 if (cfg.model == W.NODE2VEC and not cfg.deterministic) else 16}
+           # bytes per pool slot of the edge-record table: 8 (compact), 16, or 32 (node2vec MH: the
+           # footprint counts the anchor half of those records as samplers)
+           "record_bytes": record_bytes_per_slot(gs, ns, cfg.model == W.NODE2VEC and not cfg.deterministic)}
     if scan:
         res["scan_only_median_ms"] = round(float(np.median(scan)), 4)
     gs.destroy()
