@@ -1565,23 +1565,31 @@ __global__ __launch_bounds__(1024, 8) void k_rewalk_scan_lean(WalkArgs a)
 
 // k_rewalk_plan on the lean scan (round 3): 1024-thread workgroups (the 64-KiB
 // filter, two per CU), four 256-walk blocks per step, each binned and listed
-// exactly as k_rewalk_plan does it.
-template <bool NTL>
+// exactly as k_rewalk_plan does it.  FROM_AFF (round 6, A/B: WHARF_PLAN_SPLIT=1):
+// the points come from k_rewalk_scan_lean's aff[] instead, in a binning pass that
+// reads one byte per walk.  The idea was that the fused scan's binning barriers
+// hold each workgroup to its slowest wave.  The scan alone was measured as slow
+// as the fused plan (configs[4]: 5.75 vs 5.9 ms), so the split is not the default.
+template <bool NTL, bool FROM_AFF = false>
 __global__ __launch_bounds__(1024, 8) void k_rewalk_plan_lean(WalkArgs a)
 {
-    __shared__ uint32_t s_bloom[kBigBloomWords];
+    __shared__ uint32_t s_bloom[FROM_AFF ? 1 : kBigBloomWords];
     __shared__ uint32_t s_bin[4][256];                     // count, then cursor, per rewalk point (255: none)
     __shared__ uint32_t s_wsum[4][kWavesPerBlock];
     __shared__ unsigned long long s_ticket[4];
-    filter_to_lds<2>(a, s_bloom);
+    if constexpr (!FROM_AFF) filter_to_lds<2>(a, s_bloom);
     if (blockDim.x != 1024) __builtin_trap();              // four 256-walk blocks, one bin per thread
     const uint64_t W = a.W;
     const uint32_t L = a.L, t = threadIdx.x, sb = t >> 8, tl = t & 255, lane = __lane_id(), wv = tl >> 6;
     for (uint64_t base = (uint64_t)blockIdx.x * 1024; base < W; base += (uint64_t)gridDim.x * 1024) {
         const uint64_t li = base + t;
         uint32_t p = kNoRewalk;
-        if (li < W) p = lean_point<NTL>(a, s_bloom, a.walks + uniform64(li - lane), lane);
-        if (li < W) a.aff[li] = (uint8_t)p;
+        if constexpr (FROM_AFF) {
+            if (li < W) p = a.aff[li];
+        } else {
+            if (li < W) p = lean_point<NTL>(a, s_bloom, a.walks + uniform64(li - lane), lane);
+            if (li < W) a.aff[li] = (uint8_t)p;
+        }
         if (a.scan_only) continue;
         const uint32_t key = (li < W && p + 1 < L) ? p : 255u;   // re-walking: something after the point
         // plan_group (A/B): the workgroup's 1024 walks binned as one group (bins of block 0; the
@@ -1606,7 +1614,24 @@ __global__ __launch_bounds__(1024, 8) void k_rewalk_plan_lean(WalkArgs a)
         s_bin[sb][tl] = before + incl - c;
         __syncthreads();
         const uint32_t nact = s_bin[gb][255];              // entries ranked before the "none" bin
-        if (tl == 0 && gb == sb) s_ticket[sb] = nact ? atomicAdd(a.counters + 2, (1ull << 40) | nact) : 0ull;
+        if constexpr (FROM_AFF) {
+            // one list ticket per workgroup step (4 blocks) instead of one per block: without the
+            // scan in front, the same-address atomics were this pass's bound (3.9 ms at configs[4]).
+            // Bit 40 of a block's ticket, which picks its listing direction, alternates by block.
+            if (t == 0) {
+                uint32_t c[4], tot = 0;
+#pragma unroll
+                for (uint32_t b = 0; b < 4; b++) tot += (c[b] = s_bin[b][255]);   // (plan_group: blocks 1-3 stay empty)
+                uint64_t o = tot ? (atomicAdd(a.counters + 2, (4ull << 40) | tot) & kListMask) : 0ull;
+#pragma unroll
+                for (uint32_t b = 0; b < 4; b++) {
+                    s_ticket[b] = o | ((uint64_t)(b & 1u) << 40);
+                    o += c[b];
+                }
+            }
+        } else {
+            if (tl == 0 && gb == sb) s_ticket[sb] = nact ? atomicAdd(a.counters + 2, (1ull << 40) | nact) : 0ull;
+        }
         __syncthreads();
         const uint64_t blk = (base >> 8) + sb;
         if (tl == 0 && a.bdesc && (blk << 8) < W) a.bdesc[blk] = (s_ticket[sb] & kListMask) | ((uint64_t)nact << 40);
@@ -2178,11 +2203,24 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
     const char* pk = getenv("WHARF_PLAN_KERNEL");
     const bool plan_lean = !(pk && std::string(pk) == "chunked") && a.W <= kLeanMaxW;
     const dim3 pgrid((unsigned)std::min<uint64_t>((a.W + 1023) / 1024, (uint64_t)cu_count() * 2));
+    // the lean scan's grid: a multiple of 8 workgroups (xcd_range)
+    const dim3 bgrid((std::max<unsigned>(std::min<uint64_t>((a.W + 1023) / 1024, (uint64_t)cu_count() * 2), kXcds) /
+                      kXcds) * kXcds);
+    // the node2vec plan fused (default) or as the per-wave lean scan + a binning pass (WHARF_PLAN_SPLIT=1,
+    // A/B: same-session traces, profiles/r06/plan_split: configs[4] shard 38.0 / 37.5 vs 37.0 / 37.4 ms of
+    // plan + re-walk kernels per batch, configs[2] 50.1 / 49.5 vs 49.5 / 53.9; the scan alone is as slow
+    // as the fused plan, 5.75 vs 5.9 ms at configs[4], so the extra pass does not pay)
+    const char* ps = getenv("WHARF_PLAN_SPLIT");
+    const bool plan_split = ps && *ps && atoi(ps) != 0;
     const bool cr = a.rf.compact != 0;   // compact 8-B edge records (never with node2vec MH's anchors)
 #define WHARF_LAUNCH(M, D)                                                                   \
     do {                                                                                     \
         if (rewalk && M == kNode2Vec) {                                                      \
             if (a.stage == 2) {                                                              \
+            } else if (plan_lean && plan_split) {                                            \
+                if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_scan_lean<true>), bgrid, dim3(1024), 0, s, a); \
+                else hipLaunchKernelGGL((k_rewalk_scan_lean<false>), bgrid, dim3(1024), 0, s, a); \
+                hipLaunchKernelGGL((k_rewalk_plan_lean<false, true>), pgrid, dim3(1024), 0, s, a); \
             } else if (plan_lean) {                                                          \
                 if (a.nt_rows) hipLaunchKernelGGL(k_rewalk_plan_lean<true>, pgrid, dim3(1024), 0, s, a); \
                 else hipLaunchKernelGGL(k_rewalk_plan_lean<false>, pgrid, dim3(1024), 0, s, a);  \
@@ -2239,8 +2277,6 @@ void launch_walk(const WalkArgs& a, bool rewalk, hipStream_t s)
         const char* sb = getenv("WHARF_SCAN_SMALL_BLOOM");
         const char* sk = getenv("WHARF_SCAN_KERNEL");
         const bool small = sb && atoi(sb), big = sk && std::string(sk) == "big";
-        const dim3 bgrid((std::max<unsigned>(std::min<uint64_t>((a.W + 1023) / 1024, (uint64_t)cu_count() * 2), kXcds) /
-                          kXcds) * kXcds);
         if (!small && !big && a.W <= kLeanMaxW) {
             if (a.nt_rows) hipLaunchKernelGGL((k_rewalk_scan_lean<true>), bgrid, dim3(1024), 0, s, a);
             else hipLaunchKernelGGL((k_rewalk_scan_lean<false>), bgrid, dim3(1024), 0, s, a);

@@ -516,6 +516,8 @@ def test_rewalk_and_update_paths(W, monkeypatch, path, mode):
     # node2vec plan (rewalk points + the binned re-walk list): on the lean scan (default) or k_rewalk_plan
     monkeypatch.setenv("WHARF_PLAN_KERNEL", "chunked" if path in ("flat/move", "sorted/plain-rows", "park/repack-tail")
                        else "lean")
+    # the lean plan as the per-wave scan + a binning pass over its points (default) or fused in one kernel
+    monkeypatch.setenv("WHARF_PLAN_SPLIT", "0" if path in ("sorted/slack", "block/slack", "sorted/global-move") else "1")
     # deterministic suffix copy: the 32-KiB filter folded from the 64-KiB one (default) or the 16-KiB one
     monkeypatch.setenv("WHARF_COPY_SMALL_BLOOM", "1" if path == "sorted/plain-rows" else "0")
     monkeypatch.setenv("WHARF_NO_PREINIT", no_pre)

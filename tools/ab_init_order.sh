@@ -5,6 +5,7 @@
 #   prev    the tree's library, WHARF_INIT_ORDER=0 (prev order only)
 #   lib:<n> tools/ab/lib_<n>.so (e.g. an older build)
 #   bias:<x> the tree's library, WHARF_INIT_CUR_BIAS=x (lines added to the cur-order side)
+#   env:<VAR=v> the tree's library with one environment setting
 # Logs: gpurun_out/${TAG:-initord}_<variant>_<rep>.log
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -14,12 +15,13 @@ TAG=${TAG:-initord}
 REPS=${REPS:-2}
 for rep in $(seq 1 $REPS); do
     for v in "$@"; do
-        log=gpurun_out/${TAG}_${v//:/_}_${rep}.log
+        log=gpurun_out/${TAG}_$(echo "$v" | tr ":=/" "___")_${rep}.log
         (
             case $v in
                 prev) export WHARF_INIT_ORDER=0 ;;
                 lib:*) export WHARF_LIB_PATH=tools/ab/lib_${v#lib:}.so ;;
                 bias:*) export WHARF_INIT_CUR_BIAS=${v#bias:} ;;
+                env:*) export "${v#env:}" ;;
             esac
             timeout -k 10 300 python -u tools/bigscale.py --model node2vec --wpv 10 --batches ${BATCHES:-2} --mixed \
                 --no-oracle --shard 8
