@@ -178,6 +178,31 @@ def load_traffic(tag: str):
     return None, None
 
 
+def load_requests(tag: str):
+    """L2 (TCC) requests per step of the kernel from the committed rocprofv3 PMC summary, or None."""
+    for pre in PMC_ROUNDS:
+        path = os.path.join(REPO, "profiles", f"pmc_{pre}{tag}_requests.json")
+        if os.path.exists(path):
+            try:
+                d = json.load(open(path))
+                return {"per_step": d["tcc_req_per_step"], "ceiling": d["path_ceiling_G_requests_per_s"],
+                        "source": f"profiles/pmc_{pre}{tag}_requests.json (rocprofv3 PMC pass)"}
+            except Exception:
+                pass
+    return None
+
+
+def request_rate(req, steps_per_launch: float, avg_kernel_ms: float):
+    """The kernel's L2 request rate in this run: the committed requests per step x this run's steps
+    per launch / its average launch time.  The path's random-access kernels all run at 40-47 G
+    requests/s, a tighter yardstick for a gather kernel than bytes against HBM peak."""
+    if not req or not avg_kernel_ms:
+        return None
+    rate = req["per_step"] * steps_per_launch / (avg_kernel_ms * 1e-3) / 1e9
+    return {"per_step": req["per_step"], "G_per_s": round(rate, 2), "measured_ceiling_G_per_s": req["ceiling"],
+            "source": req["source"]}
+
+
 def host_cpus():
     """What the host gives this job: nproc, the affinity set, the cgroup CPU
     quota (a GPU box shows the whole machine's CPUs but grants a share), the
@@ -1286,7 +1311,9 @@ def main():
                          # the first generation of a fresh handle (node2vec: every anchor initialised)
                          "first_generation_kernel_ms": round(warm_ms[0], 3) if warm_ms else None,
                          "gather_ceiling": gather_ceiling(steps_local / (avg_kernel_ms * 1e-3), live_ceiling, matched)
-                         if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None},
+                         if bytes_per_step == BYTES_PER_STEP_DEEPWALK else None,
+                         # L2 requests: one per step at the path's measured request-rate ceiling
+                         "l2_requests": request_rate(load_requests(tag), steps_local, avg_kernel_ms)},
             "per_gpu_of_8": per8,
             "jobs_8gpu": jobs,
             "mh_accept_rate": round(st["accepts"] / st["steps"], 5) if st["steps"] else None,
