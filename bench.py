@@ -199,7 +199,7 @@ def request_rate(req, steps_per_launch: float, avg_kernel_ms: float):
     if not req or not avg_kernel_ms:
         return None
     rate = req["per_step"] * steps_per_launch / (avg_kernel_ms * 1e-3) / 1e9
-    return {"per_step": req["per_step"], "G_per_s": round(rate, 2), "measured_ceiling_G_per_s": req["ceiling"],
+    return {"per_step": req["per_step"], "G_per_s": round(rate, 2), "path_kernels_measured_G_per_s": req["ceiling"],
             "source": req["source"]}
 
 

@@ -64,5 +64,5 @@ def test_l2_request_rate_from_the_committed_summary():
     assert req is not None and 1.0 <= req["per_step"] < 1.2 and req["source"].startswith("profiles/pmc_")
     rec = bench.request_rate(req, 3_297_052_360, 76.2)
     assert rec["G_per_s"] == pytest.approx(req["per_step"] * 3_297_052_360 / 0.0762 / 1e9, rel=1e-3)
-    assert rec["measured_ceiling_G_per_s"] == [40, 47]
+    assert rec["path_kernels_measured_G_per_s"] == [40, 47]
     assert bench.load_requests("no_such_kernel_tag") is None and bench.request_rate(None, 1, 1.0) is None
