@@ -259,6 +259,39 @@ def test_node2vec_anchors_up_front_or_lazily(W, monkeypatch, preinit_all, init):
         g0.destroy()
 
 
+@pytest.mark.parametrize("init", [1, 2])   # BURNIN, WEIGHT
+def test_up_front_init_orders_agree_on_an_rmat_graph_with_hubs(W, monkeypatch, init):
+    """The two-order up-front inits at a size where the line model itself sends hub curs' states to
+    cur order (no bias): RMAT scale 15 with the reverse-slot index forced on.  Anchors are a pure
+    function of the snapshot, so prev order only (WHARF_INIT_ORDER=0), the two orders with the
+    reverse slots verified, and the two orders unverified give the same corpus and counters, then the
+    same corpus again after an insert and a delete batch."""
+    monkeypatch.setenv("WHARF_REV", "1")
+    monkeypatch.setenv("WHARF_PREINIT_ALL", "1")
+    monkeypatch.delenv("WHARF_INIT_CUR_BIAS", raising=False)
+    n = 1 << 15
+    cfg = W.WharfConfig(walks_per_vertex=2, walk_length=24, model=1, paramP=0.5, paramQ=2.0, deterministic=False,
+                        seed=23, sampler_init=init)
+    ins = O.generate_batch_of_edges(3000, n, 41, False, False)
+    out = {}
+    for variant, order, verify in (("prev", "0", "1"), ("two-verified", "1", "1"), ("two", "1", "0")):
+        monkeypatch.setenv("WHARF_INIT_ORDER", order)
+        monkeypatch.setenv("WHARF_REV_VERIFY", verify)
+        g = W.WharfMH.from_rmat(n, 400_000, 2 * n, seed=5, config=cfg)
+        g.generate_initial_random_walks()
+        st = g.stats()
+        assert st["last_anchor_inits"] == g.number_of_edges()   # one init per state, up front
+        w0 = g.walks()
+        g.insert_edges_batch(ins, sorted=False, remove_dups=True)
+        w1 = g.walks()
+        g.delete_edges_batch(ins, sorted=False, remove_dups=True)
+        out[variant] = (w0, st["steps"], st["accepts"], w1, g.walks())
+        g.destroy()
+    for variant in ("two-verified", "two"):
+        for a, b in zip(out["prev"], out[variant]):
+            np.testing.assert_array_equal(a, b)
+
+
 def test_edge_cases_isolated_dead_ends_and_flags(W):
     # vertex 5 isolated, 6 a sink (directed edge 4->6), self loop 3->3
     off = np.array([0, 2, 4, 7, 9, 11, 11, 11], dtype=np.uint64)
